@@ -1,0 +1,116 @@
+/*
+ * turbo_mi355x.h -- C ABI of the MI355X-native LTE turbo decoder (libturbo_mi355x.so).
+ *
+ * Plain pointers and sizes only (no HIP / torch types).  Every entry point names the
+ * reference interface it replaces (/root/reference/ITTC/...).  The reference's own C++
+ * entry points (TurboCodingInit / TurboEnCoding / TurboDecoding / TurboCodingRelease /
+ * AWGN / Log_MAP_decoder) are provided on top of this ABI by libturbo_logmap_compat.so
+ * (turbo_decoder_cuda_amd/csrc/log_map_compat.cpp), see INTEGRATION.md.
+ *
+ * Status codes: 0 = TD_OK; non-zero = error, message via td_last_error() (thread-local).
+ * The reference has no return codes: it printf()s and exit(1)s (log_map.cpp:288-292,357-368).
+ */
+#ifndef TURBO_MI355X_H
+#define TURBO_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TD_ABI_VERSION 1
+
+enum td_status {
+    TD_OK = 0,
+    TD_EINVAL = 1,   /* bad argument (K, f1/f2, iterations, batch, null pointer) */
+    TD_ENOMEM = 2,   /* host or device allocation failed */
+    TD_EHIP = 3,     /* HIP runtime error (message carries hipGetErrorString) */
+    TD_ENODEV = 4    /* no MI355X (gfx950) device visible */
+};
+
+/* Jacobian used by the SISO: TYPE_DECODER of ITTC/log_map.h:26-29. */
+enum td_algo {
+    TD_ALGO_LOGMAP = 0,  /* 16-step table max* (E_algorithm, log_map.cpp:779-801) -- the reference */
+    TD_ALGO_MAXLOG = 1   /* max* = max (Max-Log-MAP, BASELINE config 3) */
+};
+
+/* Arithmetic of the decode. */
+enum td_precision {
+    TD_F64 = 0,   /* IEEE fp64 with the reference's operation order: the parity mode */
+    TD_F32 = 1    /* fp32, same schedule and op order (throughput mode) */
+};
+
+/* Code and schedule parameters.  Reference: globals source_length/f1/f2 (ITTC/main.h:6-11,
+ * main.cpp:29-37), macros N_ITERATION / TERMINATED / TYPE_DECODER (ITTC/log_map.h:24-30). */
+typedef struct td_params {
+    int K;            /* information bits per codeword, 1 <= K <= 10000 (MAX_FRAME_LENGTH) */
+    int f1, f2;       /* QPP interleaver: pi(i) = (f1*i + f2*i*i) mod K (log_map.cpp:616-624) */
+    int iterations;   /* turbo iterations (N_ITERATION) */
+    int algo;         /* enum td_algo */
+    int precision;    /* enum td_precision */
+    int device;       /* HIP device ordinal this handle is bound to */
+} td_params;
+
+typedef struct td_handle td_handle;
+
+/* Replaces TurboCodingInit (log_map.cpp:349-434): builds the trellis (gen_g_matrix 13/15 +
+ * gen_trellis), the QPP table and the max* bucket table, on `p->device`. */
+int td_create(td_handle** out, const td_params* p);
+/* Replaces TurboCodingRelease (log_map.cpp:1330-1345). */
+int td_destroy(td_handle* h);
+/* Size the device workspace for batches up to B codewords.  td_decode_device grows it on
+ * demand; call td_reserve first when the decode is captured into a hipGraph. */
+int td_reserve(td_handle* h, int B);
+
+/*
+ * Batched TurboDecoding (log_map.cpp:1146-1280) on device-resident data.
+ *   d_llr   [B][3K+12] channel LLRs in the reference stream layout (main.cpp:202 output),
+ *           double for TD_F64, float for TD_F32.  Not modified (the reference scales its
+ *           buffer by 0.5 in place, :1202-1205; the compat layer reproduces that side effect).
+ *   d_bits  all_iters ? [B][iterations][K] : [B][K]  uint8 hard decisions in natural order
+ *           (row `it` = flow_decoded + K*it of the reference, :1261-1264).
+ *   d_le    nullable, [B][iterations][2][K+3] extrinsic Le after SISO1 and SISO2
+ *           (:1234-1238, :1255-1259), same dtype as d_llr.
+ *   stream  hipStream_t (NULL = default stream).  Asynchronous; no host synchronisation.
+ */
+int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
+                     void* stream);
+
+/* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
+ *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)
+ *   le   nullable host [B][iterations][2][K+3]. */
+int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le);
+
+/*
+ * Batched Log_MAP_decoder (log_map.cpp:898-1047) -- the SISO, host pointers.
+ *   recs [B][2L] (ys, yp) pairs, La [B][L], LLR [B][L] out; dtype by h's precision.
+ *   terminated: 1 = beta starts in state 0 (TERMINATED, log_map.h:24), 0 = all states equal.
+ */
+int td_siso_host(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B);
+
+/* Last error message of this thread ("" if none). */
+const char* td_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU; never fails). */
+int td_device_count(void);
+/* ABI version of the loaded library (TD_ABI_VERSION). */
+int td_abi_version(void);
+
+/*
+ * Host evaluation of the exact bucket form of E_algorithm used on the device (no GPU needed):
+ * max(x,y) + table(|y-x|) through the 72-entry LUT the kernels read from LDS.  Lets CPU
+ * tests prove LUT == log_map.cpp:779-801 for every threshold.  algo = enum td_algo.
+ */
+double td_maxstar_host_f64(double x, double y, int algo);
+float td_maxstar_host_f32(float x, float y, int algo);
+
+/* Trellis tables as built by td_create's gen_trellis restatement: nextstat[8][2],
+ * laststat[8][2], nextout[8][4] (ITTC/log_map.h:58-66). For tests. */
+int td_trellis_tables(int* nextstat, int* laststat, int* nextout);
+/* QPP permutation exactly as gen_qpp_index (log_map.cpp:616-624). For tests. */
+int td_qpp_table(int K, int f1, int f2, int* pi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,376 @@
+// td_api.cpp -- the C ABI of libturbo_mi355x.so (include/turbo_mi355x.h).
+//
+// Host side of the decoder: builds the code tables (TurboCodingInit, log_map.cpp:349-434),
+// owns the device workspace, and launches the gfx950 kernels of td_kernels.hip.  There is no
+// CPU fallback: every decode runs on an MI355X or fails with a status code.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "td_kernels.h"
+#include "td_tables.h"
+#include "turbo_mi355x.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+    return fail(TD_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define TD_HIP(call)                                   \
+    do {                                               \
+        hipError_t e_ = (call);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct td_handle {
+    td_params p{};
+    td::Trellis tr{};
+    std::vector<int> pi;
+    int* d_pi = nullptr;
+    void* d_lut = nullptr;
+    void* d_ws = nullptr;   // decode workspace
+    size_t ws_bytes = 0;
+    int ws_groups = 0;
+    size_t elem = 8;
+};
+
+namespace {
+
+template <typename T>
+void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
+{
+    std::memcpy(dp.nextstat, h->tr.nextstat, sizeof dp.nextstat);
+    std::memcpy(dp.laststat, h->tr.laststat, sizeof dp.laststat);
+    std::memcpy(dp.nextout, h->tr.nextout, sizeof dp.nextout);
+    dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
+    dp.algo = h->p.algo;
+}
+
+// Workspace carve for G groups of the handle's K.
+struct Carve {
+    size_t sys1, par1, sys2, par2, ext12, ext21, ckpt, total;
+};
+
+Carve carve(int G, int K, size_t elem)
+{
+    const int L = K + td::kMemory;
+    const int W = td::window_steps();
+    const int nT = (L + W - 1) / W;
+    const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
+    const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
+    const size_t ck = align_up((size_t)G * (nT + 1) * 64 * elem, 256);
+    Carve c{};
+    c.sys1 = 0;
+    c.par1 = c.sys1 + arrL;
+    c.sys2 = c.par1 + arrL;
+    c.par2 = c.sys2 + arrL;
+    c.ext12 = c.par2 + arrL;
+    c.ext21 = c.ext12 + arrK;
+    c.ckpt = c.ext21 + arrK;
+    c.total = c.ckpt + ck;
+    return c;
+}
+
+int ensure_ws(td_handle* h, int G)
+{
+    if (G <= h->ws_groups) return TD_OK;
+    const Carve c = carve(G, h->p.K, h->elem);
+    if (h->d_ws) {
+        TD_HIP(hipDeviceSynchronize());
+        TD_HIP(hipFree(h->d_ws));
+        h->d_ws = nullptr;
+        h->ws_groups = 0;
+    }
+    if (hipMalloc(&h->d_ws, c.total) != hipSuccess) {
+        h->d_ws = nullptr;
+        return fail(TD_ENOMEM, "hipMalloc of the decode workspace failed (" + std::to_string(c.total) + " B)");
+    }
+    h->ws_bytes = c.total;
+    h->ws_groups = G;
+    return TD_OK;
+}
+
+template <typename T>
+int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
+                    hipStream_t st)
+{
+    const int G = (B + 7) / 8;
+    int rc = ensure_ws(h, G);
+    if (rc) return rc;
+    const Carve c = carve(G, h->p.K, sizeof(T));
+    char* ws = static_cast<char*>(h->d_ws);
+    td::DecodeParams<T> dp{};
+    fill_common(dp, h);
+    dp.sys1 = reinterpret_cast<T*>(ws + c.sys1);
+    dp.par1 = reinterpret_cast<T*>(ws + c.par1);
+    dp.sys2 = reinterpret_cast<T*>(ws + c.sys2);
+    dp.par2 = reinterpret_cast<T*>(ws + c.par2);
+    dp.ext12 = reinterpret_cast<T*>(ws + c.ext12);
+    dp.ext21 = reinterpret_cast<T*>(ws + c.ext21);
+    dp.ckpt = reinterpret_cast<T*>(ws + c.ckpt);
+    dp.llr_out = nullptr;
+    dp.pi = h->d_pi;
+    dp.bits = d_bits;
+    dp.le_dump = static_cast<T*>(d_le);
+    dp.K = h->p.K;
+    dp.L = h->p.K + td::kMemory;
+    dp.nT = (dp.L + td::window_steps() - 1) / td::window_steps();
+    dp.G = G;
+    dp.B = B;
+    dp.iters = h->p.iterations;
+    dp.all_iters = all_iters ? 1 : 0;
+    hipError_t e = td::launch_decode<T>(dp, static_cast<const T*>(d_llr), st);
+    if (e != hipSuccess) return hip_fail(e, "launch_decode");
+    return TD_OK;
+}
+
+template <typename T>
+int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B)
+{
+    const int G = (B + 7) / 8;
+    const int W = td::window_steps();
+    const int nT = (L + W - 1) / W;
+    const size_t eL = (size_t)G * L * 8 * sizeof(T);
+    const size_t ck = (size_t)G * (nT + 1) * 64 * sizeof(T);
+    const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
+    char* buf = nullptr;
+    const size_t total = 4 * align_up(eL, 256) + align_up(ck, 256) + align_up(inR, 256) + 2 * align_up(inA, 256);
+    if (hipMalloc(&buf, total) != hipSuccess) return fail(TD_ENOMEM, "hipMalloc (siso) failed");
+    size_t o = 0;
+    auto take = [&](size_t n) {
+        char* p = buf + o;
+        o += align_up(n, 256);
+        return p;
+    };
+    td::DecodeParams<T> dp{};
+    fill_common(dp, h);
+    dp.sys1 = reinterpret_cast<T*>(take(eL));
+    dp.par1 = reinterpret_cast<T*>(take(eL));
+    T* la_ws = reinterpret_cast<T*>(take(eL));
+    dp.llr_out = reinterpret_cast<T*>(take(eL));
+    dp.ckpt = reinterpret_cast<T*>(take(ck));
+    T* d_recs = reinterpret_cast<T*>(take(inR));
+    T* d_la = reinterpret_cast<T*>(take(inA));
+    T* d_llr = reinterpret_cast<T*>(take(inA));
+    dp.pi = h->d_pi;
+    dp.K = L - td::kMemory;
+    dp.L = L;
+    dp.nT = nT;
+    dp.G = G;
+    dp.B = B;
+    dp.iters = 1;
+    int rc = TD_OK;
+    hipError_t e = hipMemcpy(d_recs, recs, inR, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_la, La, inA, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = td::launch_siso<T>(dp, d_recs, d_la, la_ws, terminated, d_llr, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(LLR, d_llr, inA, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = hip_fail(e, "siso");
+    (void)hipFree(buf);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* td_last_error(void) { return g_err.c_str(); }
+
+int td_abi_version(void) { return TD_ABI_VERSION; }
+
+int td_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int td_trellis_tables(int* nextstat, int* laststat, int* nextout)
+{
+    td::Trellis t;
+    if (!td::build_trellis(13, 15, t)) return fail(TD_EINVAL, "bad generator");
+    if (nextstat) std::memcpy(nextstat, t.nextstat, sizeof t.nextstat);
+    if (laststat) std::memcpy(laststat, t.laststat, sizeof t.laststat);
+    if (nextout) std::memcpy(nextout, t.nextout, sizeof t.nextout);
+    return TD_OK;
+}
+
+int td_qpp_table(int K, int f1, int f2, int* pi)
+{
+    if (K < 1 || K > 10000 || !pi) return fail(TD_EINVAL, "td_qpp_table: K out of range");
+    td::build_qpp(K, f1, f2, pi);
+    return TD_OK;
+}
+
+double td_maxstar_host_f64(double x, double y, int algo)
+{
+    static td::LutEntry<double> lut[td::kLutSize];
+    static bool init = (td::build_lut<double>(lut), true);
+    (void)init;
+    if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
+    return td::maxstar_lut<double>(x, y, lut);
+}
+
+float td_maxstar_host_f32(float x, float y, int algo)
+{
+    static td::LutEntry<float> lut[td::kLutSize];
+    static bool init = (td::build_lut<float>(lut), true);
+    (void)init;
+    if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
+    return td::maxstar_lut<float>(x, y, lut);
+}
+
+int td_create(td_handle** out, const td_params* p)
+{
+    if (!out || !p) return fail(TD_EINVAL, "td_create: null argument");
+    *out = nullptr;
+    if (p->K < 1 || p->K > 10000) return fail(TD_EINVAL, "td_create: K must be in [1, 10000] (MAX_FRAME_LENGTH)");
+    if (p->iterations < 1 || p->iterations > 64) return fail(TD_EINVAL, "td_create: iterations must be in [1, 64]");
+    if (p->algo != TD_ALGO_LOGMAP && p->algo != TD_ALGO_MAXLOG) return fail(TD_EINVAL, "td_create: bad algo");
+    if (p->precision != TD_F64 && p->precision != TD_F32) return fail(TD_EINVAL, "td_create: bad precision");
+    // the QPP table must be a permutation (gen_qpp_index does not check; a bad f1/f2 silently
+    // breaks the reference -- here it is an error)
+    std::vector<int> pi(p->K);
+    td::build_qpp(p->K, p->f1, p->f2, pi.data());
+    {
+        std::vector<char> seen(p->K, 0);
+        for (int v : pi) {
+            if (v < 0 || v >= p->K || seen[v]) return fail(TD_EINVAL, "td_create: f1/f2 do not give a QPP permutation of K");
+            seen[v] = 1;
+        }
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TD_ENODEV, "td_create: no HIP device visible");
+    if (p->device < 0 || p->device >= ndev) return fail(TD_EINVAL, "td_create: device ordinal out of range");
+    hipDeviceProp_t prop;
+    TD_HIP(hipGetDeviceProperties(&prop, p->device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(TD_ENODEV, std::string("td_create: device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+    TD_HIP(hipSetDevice(p->device));
+
+    td_handle* h = new td_handle();
+    h->p = *p;
+    h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
+    if (!td::build_trellis(13, 15, h->tr)) {   // G_ROW_1 / G_ROW_2, log_map.h:35-36
+        delete h;
+        return fail(TD_EINVAL, "td_create: bad generator");
+    }
+    h->pi = std::move(pi);
+    if (hipMalloc(&h->d_pi, sizeof(int) * p->K) != hipSuccess ||
+        hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess) {
+        td_destroy(h);
+        return fail(TD_ENOMEM, "td_create: hipMalloc failed");
+    }
+    hipError_t e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        if (p->precision == TD_F64) {
+            td::LutEntry<double> lut[td::kLutSize];
+            td::build_lut<double>(lut);
+            e = hipMemcpy(h->d_lut, lut, sizeof lut, hipMemcpyHostToDevice);
+        } else {
+            td::LutEntry<float> lut[td::kLutSize];
+            td::build_lut<float>(lut);
+            e = hipMemcpy(h->d_lut, lut, sizeof lut, hipMemcpyHostToDevice);
+        }
+    }
+    if (e != hipSuccess) {
+        td_destroy(h);
+        return hip_fail(e, "td_create: table upload");
+    }
+    *out = h;
+    return TD_OK;
+}
+
+int td_destroy(td_handle* h)
+{
+    if (!h) return TD_OK;
+    (void)hipSetDevice(h->p.device);
+    if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->d_pi) (void)hipFree(h->d_pi);
+    if (h->d_lut) (void)hipFree(h->d_lut);
+    delete h;
+    return TD_OK;
+}
+
+int td_reserve(td_handle* h, int B)
+{
+    if (!h || B < 1) return fail(TD_EINVAL, "td_reserve: bad argument");
+    TD_HIP(hipSetDevice(h->p.device));
+    return ensure_ws(h, (B + 7) / 8);
+}
+
+int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
+                     void* stream)
+{
+    if (!h || !d_llr || !d_bits || B < 1) return fail(TD_EINVAL, "td_decode_device: bad argument");
+    TD_HIP(hipSetDevice(h->p.device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (h->p.precision == TD_F64) return decode_device_t<double>(h, d_llr, B, d_bits, all_iters, d_le, st);
+    return decode_device_t<float>(h, d_llr, B, d_bits, all_iters, d_le, st);
+}
+
+int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le)
+{
+    if (!h || !llr || !out || B < 1) return fail(TD_EINVAL, "td_decode_host: bad argument");
+    TD_HIP(hipSetDevice(h->p.device));
+    const int K = h->p.K, L = K + td::kMemory, it = h->p.iterations;
+    const size_t n = 3 * (size_t)K + 4 * td::kMemory;
+    const size_t in_b = (size_t)B * n * h->elem;
+    const size_t bits_b = (size_t)B * it * K;
+    const size_t le_b = le ? (size_t)B * it * 2 * L * h->elem : 0;
+    void *d_in = nullptr, *d_le = nullptr;
+    uint8_t* d_bits = nullptr;
+    int rc = TD_OK;
+    if (hipMalloc(&d_in, in_b) != hipSuccess || hipMalloc(&d_bits, bits_b) != hipSuccess ||
+        (le && hipMalloc(&d_le, le_b) != hipSuccess)) {
+        rc = fail(TD_ENOMEM, "td_decode_host: hipMalloc failed");
+    }
+    hipError_t e = hipSuccess;
+    if (!rc) e = hipMemcpy(d_in, llr, in_b, hipMemcpyHostToDevice);
+    if (!rc && e == hipSuccess) rc = td_decode_device(h, d_in, B, d_bits, 1, d_le, nullptr);
+    if (!rc && e == hipSuccess) e = hipDeviceSynchronize();
+    std::vector<uint8_t> hb;
+    if (!rc && e == hipSuccess) {
+        hb.resize(bits_b);
+        e = hipMemcpy(hb.data(), d_bits, bits_b, hipMemcpyDeviceToHost);
+    }
+    if (!rc && e == hipSuccess && le) e = hipMemcpy(le, d_le, le_b, hipMemcpyDeviceToHost);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "td_decode_host");
+    if (!rc)
+        for (size_t i = 0; i < bits_b; ++i) out[i] = hb[i];
+    if (d_in) (void)hipFree(d_in);
+    if (d_bits) (void)hipFree(d_bits);
+    if (d_le) (void)hipFree(d_le);
+    return rc;
+}
+
+int td_siso_host(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B)
+{
+    if (!h || !recs || !La || !LLR || L < 1 || B < 1) return fail(TD_EINVAL, "td_siso_host: bad argument");
+    TD_HIP(hipSetDevice(h->p.device));
+    int rc = h->p.precision == TD_F64 ? siso_host_t<double>(h, recs, La, terminated, LLR, L, B)
+                                      : siso_host_t<float>(h, recs, La, terminated, LLR, L, B);
+    if (!rc) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return hip_fail(e, "td_siso_host");
+    }
+    return rc;
+}
+
+}  // extern "C"

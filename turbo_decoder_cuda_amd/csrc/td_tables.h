@@ -1,0 +1,163 @@
+// td_tables.h -- code tables shared by the host API and the gfx950 kernels.
+//
+//  * trellis of the LTE 8-state RSC, built from the octal generators exactly as
+//    gen_g_matrix/gen_trellis do (ITTC/log_map.cpp:114-169, 247-269, 281-337);
+//  * the QPP permutation (gen_qpp_index, log_map.cpp:616-624);
+//  * the max* bucket table: an exact, branch-free form of E_algorithm's 16-step linear
+//    scan (log_map.cpp:14-18, 779-801).  d = |y - x| is split into 1/16-wide buckets; no
+//    bucket holds more than one threshold (smallest gap 0.08824 > 1/16), so
+//        f(d) = (d >= thr[q]) ? vhi[q] : vlo[q],   q = min(floor(16 d), 71)
+//    reproduces the reference's table value for every double (or float) d >= 0.
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+
+namespace td {
+
+constexpr int kStates = 8;
+constexpr int kMemory = 3;        // M_num_reg (log_map.cpp:28)
+constexpr int kLutSize = 72;      // buckets 0..71 (71 = every d >= 71/16)
+constexpr double kInfty = 1e20;   // INFTY (log_map.h:74-76)
+
+// log_map.cpp:14-18
+constexpr double kIdx[16] = {0.0,    0.08824, 0.19587, 0.31026, 0.43275, 0.56508, 0.70963, 0.86972,
+                             1.0502, 1.2587,  1.5078,  1.8212,  2.2522,  2.9706,  3.6764,  4.3758};
+constexpr double kTab[16] = {0.69315, 0.65, 0.6, 0.55, 0.5, 0.45, 0.4, 0.35,
+                             0.3,     0.25, 0.2, 0.15, 0.1, 0.05, 0.025, 0.0125};
+
+template <typename T>
+struct alignas(4 * sizeof(T)) LutEntry {
+    T thr, vlo, vhi, pad;
+};
+
+// Trellis (TURBO_TRELLIS, log_map.h:58-66) plus the per-state constants the kernels use.
+struct Trellis {
+    int nextout[kStates][4];
+    int nextstat[kStates][2];
+    int lastout[kStates][4];
+    int laststat[kStates][2];
+};
+
+// gen_g_matrix (log_map.cpp:114-169): octal -> 4 binary taps, MSB first. false on a non-octal digit.
+inline bool octal_taps(int g, int* taps)
+{
+    for (int j = 0; j < 4; ++j) taps[j] = 0;
+    int pos = 1, i = 0;
+    while (g > 0) {
+        int low = g % 10;
+        if (low > 7) return false;
+        g /= 10;
+        for (i = 4 - (pos - 1) * 3 - 1; i >= 0 && i >= 4 - pos * 3; --i) {
+            taps[i] = low % 2;
+            low /= 2;
+        }
+        ++pos;
+        if (i < 0) break;
+    }
+    return true;
+}
+
+// gen_trellis (log_map.cpp:281-337) for generators (feedback, forward) in octal.
+inline bool build_trellis(int g_fb_oct, int g_ff_oct, Trellis& t)
+{
+    int fb[4], ff[4];
+    if (!octal_taps(g_fb_oct, fb) || !octal_taps(g_ff_oct, ff)) return false;
+    for (int s = 0; s < kStates; ++s) {
+        for (int u = 0; u < 2; ++u) {
+            int st[3] = {(s >> 2) & 1, (s >> 1) & 1, s & 1};   // int2bin, MSB first
+            int ak = fb[0] * u;
+            for (int k = 1; k < 4; ++k) ak += fb[k] * st[k - 1];
+            ak %= 2;
+            int out = ff[0] * ak;   // encode_bit, log_map.cpp:247-269
+            for (int j = 1; j < 4; ++j) out = (out + ff[j] * st[j - 1]) % 2;
+            st[2] = st[1];
+            st[1] = st[0];
+            st[0] = ak;
+            t.nextout[s][2 * u] = 2 * u - 1;
+            t.nextout[s][2 * u + 1] = 2 * out - 1;
+            t.nextstat[s][u] = st[0] * 4 + st[1] * 2 + st[2];
+        }
+    }
+    for (int s = 0; s < kStates; ++s)
+        for (int u = 0; u < 2; ++u) {
+            int ns = t.nextstat[s][u];
+            t.laststat[ns][u] = s;
+            t.lastout[ns][2 * u] = t.nextout[s][2 * u];
+            t.lastout[ns][2 * u + 1] = t.nextout[s][2 * u + 1];
+        }
+    return true;
+}
+
+// gen_qpp_index (log_map.cpp:616-624), int32 arithmetic as the reference (valid for K <= 10000).
+inline void build_qpp(int K, int f1, int f2, int* pi)
+{
+    for (int i = 0; i < K; ++i) pi[i] = (f1 * i + (((f2 * i) % K) * i) % K) % K;
+}
+
+// The bucket table for precision T.  Thresholds and values are the reference's doubles
+// rounded once to T (exact for T = double).
+template <typename T>
+inline void build_lut(LutEntry<T>* lut)
+{
+    T thr[16], val[16];
+    for (int k = 0; k < 16; ++k) {
+        thr[k] = (T)kIdx[k];
+        val[k] = (T)kTab[k];
+    }
+    val[15] = (T)0;   // d >= idx[15] -> 0 (log_map.cpp:784-787); table[15] is unreachable
+    for (int q = 0; q < kLutSize; ++q) {
+        int base = 0, in_bucket = -1;
+        for (int k = 1; k < 16; ++k) {
+            double fl = std::floor((double)thr[k] * 16.0);
+            if (fl < q) ++base;
+            if ((int)fl == q) in_bucket = k;
+        }
+        lut[q].thr = in_bucket >= 0 ? thr[in_bucket] : (T)INFINITY;
+        lut[q].vlo = val[base];
+        lut[q].vhi = val[base + 1 <= 15 ? base + 1 : 15];
+        lut[q].pad = (T)0;
+    }
+}
+
+// Bucket max*, host/device.  fabs(y-x) equals the reference's (y-x)>0?(y-x):(x-y) exactly
+// (IEEE negation is exact), and max(x,y) equals x>y?x:y for every non-NaN pair.
+template <typename T>
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline T bucket_index_clamp(T d);
+
+template <>
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline double bucket_index_clamp<double>(double d)
+{
+    return fmin(d * 16.0, 71.0);
+}
+
+template <>
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline float bucket_index_clamp<float>(float d)
+{
+    return fminf(d * 16.0f, 71.0f);
+}
+
+template <typename T>
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline T maxstar_lut(T x, T y, const LutEntry<T>* lut)
+{
+    T d = y - x;
+    d = d < (T)0 ? -d : d;
+    T m = x > y ? x : y;
+    int q = (int)bucket_index_clamp<T>(d);
+    const LutEntry<T> e = lut[q];
+    return m + (d >= e.thr ? e.vhi : e.vlo);
+}
+
+}  // namespace td

@@ -1,0 +1,135 @@
+"""Host-side mirror of the reference codec interface (ITTC/log_map.cpp), over the C ABI.
+
+Reference                                   here
+  TurboCodingInit()          :349-434   ->  TurboCodec(K, f1, f2, iterations, algo, precision, device)
+  TurboDecoding(flow,out,n)  :1146-1280 ->  TurboCodec.TurboDecoding(flow)  (host arrays, batched)
+                                            TurboCodec.decode(llr_tensor)   (device-resident, batched)
+  Log_MAP_decoder(...)       :898-1047  ->  TurboCodec.Log_MAP_decoder(recs, La, terminated)
+  TurboCodingRelease()       :1330-1345 ->  TurboCodec.close()
+  N_ITERATION (log_map.h:30)            ->  `iterations` (runtime, default 15 like the macro)
+  TYPE_DECODER (log_map.h:26)           ->  `algo` ("logmap" = table max*, "maxlog")
+
+Every decode runs on the MI355X through libturbo_mi355x.so; nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+N_ITERATION = 15   # log_map.h:30
+TERMINATED = 1     # log_map.h:24
+
+_ALGOS = {"logmap": N.TD_ALGO_LOGMAP, "maxlog": N.TD_ALGO_MAXLOG}
+_PRECS = {"f64": N.TD_F64, "f32": N.TD_F32}
+
+
+def stream_length(K: int) -> int:
+    """3K+12: the coded stream length TurboDecoding takes (main.cpp:221)."""
+    return 3 * K + 12
+
+
+class TurboCodec:
+    def __init__(self, K: int, f1: int, f2: int, iterations: int = N_ITERATION, algo: str = "logmap",
+                 precision: str = "f64", device: int = 0):
+        self.K, self.f1, self.f2 = int(K), int(f1), int(f2)
+        self.L = self.K + 3
+        self.iterations = int(iterations)
+        self.algo, self.precision = algo, precision
+        self.dtype = np.float64 if precision == "f64" else np.float32
+        p = N.TdParams(self.K, self.f1, self.f2, self.iterations, _ALGOS[algo], _PRECS[precision], int(device))
+        h = C.c_void_p()
+        N.check(N.lib().td_create(C.byref(h), C.byref(p)))
+        self._h = h
+        self.device = int(device)
+
+    # -- lifetime (TurboCodingRelease) -------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.lib().td_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def reserve(self, B: int) -> None:
+        N.check(N.lib().td_reserve(self._h, int(B)))
+
+    # -- TurboDecoding, host arrays ------------------------------------------------------
+    def TurboDecoding(self, flow: np.ndarray, return_le: bool = False):
+        """flow [B, 3K+12] (or one row) -> out int32 [B, iterations, K] (the reference's
+        flow_decoded rows); with return_le also Le [B, iterations, 2, K+3]."""
+        flow = np.ascontiguousarray(flow, dtype=self.dtype)
+        one = flow.ndim == 1
+        flow = flow.reshape(-1, stream_length(self.K))
+        B = flow.shape[0]
+        out = np.zeros((B, self.iterations, self.K), dtype=np.int32)
+        le = np.zeros((B, self.iterations, 2, self.L), dtype=self.dtype) if return_le else None
+        N.check(N.lib().td_decode_host(self._h, flow.ctypes.data_as(C.c_void_p), B,
+                                       out.ctypes.data_as(C.c_void_p),
+                                       le.ctypes.data_as(C.c_void_p) if return_le else None))
+        if one:
+            out, le = out[0], (le[0] if return_le else None)
+        return (out, le) if return_le else out
+
+    # -- device-resident decode (torch tensors as HBM buffers) ---------------------------
+    def decode(self, llr, bits=None, all_iters: bool = False, le=None, stream=None):
+        """llr: torch tensor [B, 3K+12] on this codec's device (float64 for f64, float32 for f32).
+        Returns uint8 bits [B, K] (or [B, iterations, K] with all_iters).  Asynchronous on
+        `stream` (default: torch's current stream)."""
+        import torch
+
+        want = torch.float64 if self.precision == "f64" else torch.float32
+        if llr.dtype != want or not llr.is_cuda or not llr.is_contiguous():
+            raise ValueError(f"llr must be a contiguous {want} CUDA tensor")
+        B = llr.shape[0]
+        if bits is None:
+            shape = (B, self.iterations, self.K) if all_iters else (B, self.K)
+            bits = torch.empty(shape, dtype=torch.uint8, device=llr.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(llr.device)
+        N.check(N.lib().td_decode_device(self._h, C.c_void_p(llr.data_ptr()), B, C.c_void_p(bits.data_ptr()),
+                                         int(all_iters), C.c_void_p(le.data_ptr()) if le is not None else None,
+                                         C.c_void_p(stream.cuda_stream)))
+        return bits
+
+    def decode_raw(self, llr_ptr: int, B: int, bits_ptr: int, all_iters: bool = False, le_ptr: int = 0,
+                   stream_ptr: int = 0) -> None:
+        N.check(N.lib().td_decode_device(self._h, C.c_void_p(llr_ptr), int(B), C.c_void_p(bits_ptr),
+                                         int(all_iters), C.c_void_p(le_ptr) if le_ptr else None,
+                                         C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    # -- Log_MAP_decoder -----------------------------------------------------------------
+    def Log_MAP_decoder(self, recs: np.ndarray, La: np.ndarray, terminated: int = TERMINATED) -> np.ndarray:
+        """recs [B, 2L] (ys, yp pairs), La [B, L] -> LLR [B, L] (or 1-D for one codeword)."""
+        recs = np.ascontiguousarray(recs, dtype=self.dtype)
+        La = np.ascontiguousarray(La, dtype=self.dtype)
+        one = La.ndim == 1
+        La2 = La.reshape(1, -1) if one else La
+        L = La2.shape[1]
+        recs2 = recs.reshape(-1, 2 * L)
+        B = La2.shape[0]
+        out = np.zeros((B, L), dtype=self.dtype)
+        N.check(N.lib().td_siso_host(self._h, recs2.ctypes.data_as(C.c_void_p), La2.ctypes.data_as(C.c_void_p),
+                                     int(terminated), out.ctypes.data_as(C.c_void_p), L, B))
+        return out[0] if one else out
+
+
+def TurboCodingInit(K: int, f1: int, f2: int, **kw) -> TurboCodec:
+    """Reference-named constructor (log_map.cpp:349): parameters explicit instead of globals."""
+    return TurboCodec(K, f1, f2, **kw)
+
+
+def device_count() -> int:
+    return N.lib().td_device_count()
