@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X turbo decoder -- BASELINE.json metric:
+    decoded info Mbit/s @ K=6144, 8 iter, Eb/N0=1.0 dB; BER match vs CPU log_map
+
+Workload at N=1 = BASELINE config 2: batch 4096 x K=6144, 8 log-MAP (table max*) iterations,
+rate 1/3, fp64 parity arithmetic (the reference's precision and operation order).
+A "step" = one td_decode_device call on the resident batch (demultiplex + all iterations +
+hard decisions).  N>1: one process per GPU (torchrun), each decodes its own 4096-codeword
+shard -- weak scaling, no data-path collective; the only exchange is the max of the step
+times and the sum of error counters (gloo, host scalars).
+
+Extra objects on the JSON line:
+  roofline      the turbo kernel against HBM (algorithmic bytes: fp64 LLR in + uint8 bits out
+                per codeword) with durations from hipEvents inside the timed region;
+                `traffic` from the committed rocprofv3 PMC profile of the same config (or null)
+  cpu_baseline  oracle/ (CPU restatement of log_map.cpp, fp64) on the host cores, rank 0, N=1
+  variants      fp32 log-MAP, fp64/fp32 Max-Log-MAP on the same batch (fewer steps)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "decoded info Mbit/s @ K=6144, 8 iter, Eb/N0=1.0 dB; BER match vs CPU log_map"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (half the FP32 vector rate, 157.3 TF)
+F1, F2 = 263, 480             # QPP for K=6144 (ITTC/main.cpp:36-37)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4096, help="codewords per GPU")
+    ap.add_argument("--K", type=int, default=6144)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--ebn0", type=float, default=1.0)
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
+    ap.add_argument("--cpu-sample", type=int, default=256, help="codewords for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-variants", action="store_true")
+    return ap.parse_args()
+
+
+def qpp_for(K):
+    if K == 6144:
+        return F1, F2
+    if K == 1024:
+        return 31, 64
+    if K == 40:
+        return 3, 10
+    raise SystemExit("bench: give K in {40, 1024, 6144}")
+
+
+def load_traffic(cfg_key):
+    """HBM bytes per turbo-kernel launch from profiles/traffic.json (rocprofv3 PMC, committed)."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(cfg_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    from turbo_decoder_cuda_amd import TurboCodec, synth
+
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    f1, f2 = qpp_for(a.K)
+    np_dt = np.float64 if a.precision == "f64" else np.float32
+    u, llr_h = synth.make_batch(a.batch, a.K, f1, f2, a.ebn0, seed=20261015 + rank, dtype=np.float64)
+    llr64 = torch.from_numpy(llr_h).to(dev)
+    llr = llr64 if a.precision == "f64" else llr64.float()
+    u_d = torch.from_numpy(u).to(dev)
+
+    codec = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=local)
+    codec.reserve(a.batch)
+    bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        codec.decode(llr, bits, stream=stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+
+    codec.profile(True)   # hipEvents around each kernel, inside the timed region
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        codec.decode(llr, bits, stream=stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    barrier()
+    demux_ms, turbo_ms, nlaunch = codec.kernel_ms()
+    codec.profile(False)
+
+    elapsed = t1 - t0
+    errs = int((bits != u_d).sum().item())
+    blk = int((bits != u_d).any(dim=1).sum().item())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([errs, blk], dtype=torch.int64)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        errs, blk = int(e[0]), int(e[1])
+
+    ms_step = elapsed / a.steps * 1e3
+    total_bits = world * a.batch * a.K * a.steps
+    value = total_bits / elapsed / 1e6
+    esz = 8 if a.precision == "f64" else 4
+    bytes_cw = esz * (3 * a.K + 12) + a.K   # algorithmic: LLR in + uint8 bits out
+    alg_bytes = bytes_cw * a.batch
+    achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9
+    cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}"
+    traffic = load_traffic(cfg_key)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mbit/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": a.precision,
+        "data": "synthetic: PCG64 info bits, RSC 13/15 + QPP turbo encoder, BPSK, AWGN (numpy), LLR=2y/sigma^2",
+        "config": {
+            "workload": f"BASELINE config {'2' if a.algo == 'logmap' else '3'}: batch {a.batch} x K={a.K} per GPU, "
+                        f"{a.iters} iterations, {'log-MAP table max*' if a.algo == 'logmap' else 'Max-Log-MAP'}, "
+                        f"{a.precision} {'parity (reference op order)' if a.precision == 'f64' else 'throughput'}, "
+                        f"Eb/N0={a.ebn0} dB",
+            "K": a.K, "f1": f1, "f2": f2, "batch_per_gpu": a.batch, "global_batch": a.batch * world,
+            "iterations": a.iters, "algo": a.algo, "precision": a.precision, "ebn0_db": a.ebn0,
+            "parallelism": f"batch-shard x{world} (no collective on the data path)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "turbo_decode_kernel",
+            "achieved": round(achieved, 3),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6),
+            "traffic": traffic,
+            "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_per_codeword": bytes_cw,
+            "kernel_ms_avg": round(turbo_ms, 4),
+            "demux_ms_avg": round(demux_ms, 4),
+            "launches_timed": nlaunch,
+        },
+        "ber": {"bit_errors": errs, "block_errors": blk,
+                "ber": errs / (world * a.batch * a.K), "bler": blk / (world * a.batch)},
+    }
+
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(a, llr_h, bits.cpu().numpy(), f1, f2)
+    if rank == 0 and world == 1 and not a.no_variants:
+        out["variants"] = variants(a, llr64, u_d, f1, f2, dev, stream)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, llr_h, gpu_bits, f1, f2):
+    """The CPU restatement of log_map.cpp (oracle/, fp64 table log-MAP -- the reference's own
+    arithmetic) on the host cores, over the first `cpu_sample` codewords of the same batch."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+
+    n = min(a.cpu_sample, a.batch)
+    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    sample = np.ascontiguousarray(llr_h[:n])
+    if a.precision == "f32":
+        sample = sample.astype(np.float32)
+    algo = pyoracle.ALGO_LOGMAP if a.algo == "logmap" else pyoracle.ALGO_MAXLOG
+    t0 = time.perf_counter()
+    cb = pyoracle.decode_batch(sample, a.K, f1, f2, a.iters, algo, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(n * a.K / dt / 1e6, 4),
+        "unit": "Mbit/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} codewords of the same batch (K={a.K}, {a.iters} iter, {a.precision} {a.algo}), "
+                  f"{threads} threads, {dt:.2f} s",
+        "bits_match_gpu": bool(np.array_equal(cb, gpu_bits[:n])),
+        "cpu_model": _cpu_model(),
+    }
+
+
+def variants(a, llr64, u_d, f1, f2, dev, stream):
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+
+    res = {}
+    for prec, algo in (("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog")):
+        if prec == a.precision and algo == a.algo:
+            continue
+        x = llr64 if prec == "f64" else llr64.float()
+        c = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=algo, precision=prec, device=dev.index)
+        c.reserve(a.batch)
+        b = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
+        c.decode(x, b, stream=stream)
+        torch.cuda.synchronize(dev)
+        steps = max(2, a.steps // 2)
+        c.profile(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            c.decode(x, b, stream=stream)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        _, kms, _ = c.kernel_ms()
+        c.close()
+        errs = int((b != u_d).sum().item())
+        res[f"{prec}_{algo}"] = {"value": round(a.batch * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s",
+                                 "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4),
+                                 "bit_errors": errs}
+    return res
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

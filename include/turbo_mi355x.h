@@ -77,6 +77,13 @@ int td_reserve(td_handle* h, int B);
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                      void* stream);
 
+/* Kernel timing (measurement support): while enabled, hipEvents on the decode stream bracket
+ * the demultiplex kernel and the turbo kernel of every td_decode_device call.
+ * td_profile_read synchronises on them, returns the average durations (ms) over the
+ * `launches` decodes since the last read/enable, and starts a new accumulation. */
+int td_profile_enable(td_handle* h, int on);
+int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches);
+
 /* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
  *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)
  *   le   nullable host [B][iterations][2][K+3]. */

@@ -19,7 +19,7 @@ TD_F64, TD_F32 = 0, 1
 EXPORTS = (
     "td_create", "td_destroy", "td_reserve", "td_decode_device", "td_decode_host", "td_siso_host",
     "td_last_error", "td_device_count", "td_abi_version", "td_maxstar_host_f64", "td_maxstar_host_f32",
-    "td_trellis_tables", "td_qpp_table",
+    "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read",
 )
 
 
@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
     L.td_maxstar_host_f32.restype = C.c_float
     L.td_trellis_tables.argtypes = [P, P, P]
     L.td_qpp_table.argtypes = [I, I, I, P]
+    L.td_profile_enable.argtypes = [P, I]
+    L.td_profile_read.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
     _lib = L
     return L
 

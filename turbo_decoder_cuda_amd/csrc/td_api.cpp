@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
+#include <array>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -49,6 +50,9 @@ struct td_handle {
     size_t ws_bytes = 0;
     int ws_groups = 0;
     size_t elem = 8;
+    bool prof = false;          // td_profile_enable
+    std::vector<std::array<hipEvent_t, 3>> ev;   // one triple per profiled decode
+    size_t nev = 0;
 };
 
 namespace {
@@ -136,8 +140,22 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.B = B;
     dp.iters = h->p.iterations;
     dp.all_iters = all_iters ? 1 : 0;
-    hipError_t e = td::launch_decode<T>(dp, static_cast<const T*>(d_llr), st);
-    if (e != hipSuccess) return hip_fail(e, "launch_decode");
+    hipEvent_t* ev = nullptr;
+    if (h->prof) {
+        if (h->nev == h->ev.size()) {
+            std::array<hipEvent_t, 3> tri{};
+            for (auto& x : tri) TD_HIP(hipEventCreate(&x));
+            h->ev.push_back(tri);
+        }
+        ev = h->ev[h->nev++].data();
+        TD_HIP(hipEventRecord(ev[0], st));
+    }
+    hipError_t e = td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
+    if (e != hipSuccess) return hip_fail(e, "launch_demux");
+    if (ev) TD_HIP(hipEventRecord(ev[1], st));
+    e = td::launch_turbo<T>(dp, st);
+    if (e != hipSuccess) return hip_fail(e, "launch_turbo");
+    if (ev) TD_HIP(hipEventRecord(ev[2], st));
     return TD_OK;
 }
 
@@ -304,6 +322,8 @@ int td_destroy(td_handle* h)
     if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->d_pi) (void)hipFree(h->d_pi);
     if (h->d_lut) (void)hipFree(h->d_lut);
+    for (auto& tri : h->ev)
+        for (auto& e : tri) (void)hipEventDestroy(e);
     delete h;
     return TD_OK;
 }
@@ -323,6 +343,35 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (h->p.precision == TD_F64) return decode_device_t<double>(h, d_llr, B, d_bits, all_iters, d_le, st);
     return decode_device_t<float>(h, d_llr, B, d_bits, all_iters, d_le, st);
+}
+
+int td_profile_enable(td_handle* h, int on)
+{
+    if (!h) return fail(TD_EINVAL, "td_profile_enable: null handle");
+    h->prof = on != 0;
+    h->nev = 0;
+    return TD_OK;
+}
+
+int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches)
+{
+    if (!h || !h->prof) return fail(TD_EINVAL, "td_profile_read: profiling not enabled");
+    TD_HIP(hipSetDevice(h->p.device));
+    double sa = 0, sb = 0;
+    for (size_t k = 0; k < h->nev; ++k) {
+        float a = 0, b = 0;
+        TD_HIP(hipEventSynchronize(h->ev[k][2]));
+        TD_HIP(hipEventElapsedTime(&a, h->ev[k][0], h->ev[k][1]));
+        TD_HIP(hipEventElapsedTime(&b, h->ev[k][1], h->ev[k][2]));
+        sa += a;
+        sb += b;
+    }
+    const int n = (int)h->nev;
+    if (demux_ms) *demux_ms = n ? (float)(sa / n) : 0.f;
+    if (decode_ms) *decode_ms = n ? (float)(sb / n) : 0.f;
+    if (launches) *launches = n;
+    h->nev = 0;
+    return TD_OK;
 }
 
 int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le)

@@ -31,8 +31,12 @@ struct DecodeParams {
     int nextout[kStates][4];
 };
 
+// demultiplex + x0.5 of the stream into the batch-interleaved arrays
 template <typename T>
-hipError_t launch_decode(const DecodeParams<T>& p, const T* flow, hipStream_t st);
+hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st);
+// the turbo iterations (one wave per 8 codewords)
+template <typename T>
+hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st);
 
 template <typename T>
 hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* la_ws, int terminated, T* llr,

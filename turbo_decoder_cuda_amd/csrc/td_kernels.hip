@@ -431,12 +431,18 @@ __global__ __launch_bounds__(256) void siso_out_kernel(DecodeParams<T> p, T* llr
 
 // ------------------------------------------------------------------ launchers
 template <typename T>
-hipError_t launch_decode(const DecodeParams<T>& p, const T* flow, hipStream_t st)
+hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 {
     const size_t total = (size_t)p.G * p.L * kCw;
     int gblocks = (int)((total + 255) / 256);
     if (gblocks > 8192) gblocks = 8192;
     hipLaunchKernelGGL(demux_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, flow);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st)
+{
     if (p.algo == 1)
         hipLaunchKernelGGL((turbo_decode_kernel<T, 1>), dim3(p.G), dim3(kLanes), 0, st, p);
     else
@@ -460,8 +466,10 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
     return hipGetLastError();
 }
 
-template hipError_t launch_decode<double>(const DecodeParams<double>&, const double*, hipStream_t);
-template hipError_t launch_decode<float>(const DecodeParams<float>&, const float*, hipStream_t);
+template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
+template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
+template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t);
+template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);
 template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*, const float*, float*, int, float*,

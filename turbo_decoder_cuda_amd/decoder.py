@@ -110,6 +110,18 @@ class TurboCodec:
                                          int(all_iters), C.c_void_p(le_ptr) if le_ptr else None,
                                          C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    # -- measurement ---------------------------------------------------------------------
+    def profile(self, on: bool = True) -> None:
+        """Bracket the next decodes' kernels with hipEvents (see td_profile_enable)."""
+        N.check(N.lib().td_profile_enable(self._h, int(on)))
+
+    def kernel_ms(self):
+        """(demux_ms, turbo_ms, launches): average kernel durations over the decodes since the
+        last call (synchronises on their events)."""
+        a, b, n = C.c_float(), C.c_float(), C.c_int()
+        N.check(N.lib().td_profile_read(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
     # -- Log_MAP_decoder -----------------------------------------------------------------
     def Log_MAP_decoder(self, recs: np.ndarray, La: np.ndarray, terminated: int = TERMINATED) -> np.ndarray:
         """recs [B, 2L] (ys, yp pairs), La [B, L] -> LLR [B, L] (or 1-D for one codeword)."""
