@@ -84,6 +84,12 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
 int td_profile_enable(td_handle* h, int on);
 int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches);
 
+/* Diagnostics: in a library built with -DTD_STAMPS (td_debug_stamp_slots() > 0) the turbo
+ * kernel writes per-wave shader-clock totals of its phases into d_buf [ceil(B/8)][slots]
+ * (uint64).  The production library ignores the buffer and reports 0 slots. */
+int td_debug_set_stamps(td_handle* h, void* d_buf);
+int td_debug_stamp_slots(void);
+
 /* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
  *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)
  *   le   nullable host [B][iterations][2][K+3]. */

@@ -1,0 +1,40 @@
+"""Diagnostic: per-wave cycle split of the turbo kernel (TD_STAMPS build).
+Usage on the GPU box: python scripts/diag_stamps.py [B] [precision] [algo]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["TD_LIB_PATH"] = os.path.join(REPO, "turbo_decoder_cuda_amd", "libturbo_mi355x_stamps.so")
+sys.path.insert(0, REPO)
+import ctypes as C  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from turbo_decoder_cuda_amd import TurboCodec, synth  # noqa: E402
+from turbo_decoder_cuda_amd import _native as N  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+prec = sys.argv[2] if len(sys.argv) > 2 else "f64"
+algo = sys.argv[3] if len(sys.argv) > 3 else "logmap"
+K, iters = 6144, 8
+u, llr = synth.make_batch(B, K, 263, 480, 1.0, dtype=np.float64 if prec == "f64" else np.float32)
+x = torch.from_numpy(llr).cuda()
+c = TurboCodec(K, 263, 480, iterations=iters, precision=prec, algo=algo)
+slots = N.lib().td_debug_stamp_slots()
+G = (B + 7) // 8
+st = torch.zeros((G, slots), dtype=torch.int64, device="cuda")
+N.check(N.lib().td_debug_set_stamps(c._h, C.c_void_p(st.data_ptr())))
+bits = c.decode(x)
+torch.cuda.synchronize()
+c.profile(True)
+bits = c.decode(x)
+_, kms, _ = c.kernel_ms()
+s = st.cpu().numpy().reshape(G, 4, 7).astype(np.float64)
+L = K + 3
+steps = 2 * iters * L
+print(f"B={B} {prec} {algo} kernel_ms={kms:.3f} errs={int((bits.cpu().numpy() != u).sum())}")
+roles = ["A alpha", "B beta", "F0 fold+load", "F1 fold"]
+for w in range(4):
+    fw, fwait, bw, bwait = (s[:, w, i].mean() / steps for i in range(4))
+    print(f"  {roles[w]:14s} per SISO-step: F work {fw:7.1f}  F wait {fwait:7.1f}  B work {bw:7.1f}  B wait {bwait:7.1f}")

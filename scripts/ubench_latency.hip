@@ -1,0 +1,123 @@
+// ubench_latency.hip -- dependent-chain latencies on gfx950 for the operations on the turbo
+// decoder's recursion (one wave per workgroup, 64 workgroups).  Prints cycles per chained op.
+// hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-honor-nans -o ubench scripts/ubench_latency.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define N 4096
+
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v)
+{
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+__global__ void k(double* out, double a, unsigned long long* cyc, int mode)
+{
+    __shared__ double lds[64 * 4];
+    for (int i = threadIdx.x; i < 256; i += 64) lds[i] = 1e-9 * i;
+    __syncthreads();
+    double x = a * (threadIdx.x + 1);
+    float xf = (float)x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    switch (mode) {
+        case 0:   // v_add_f64
+            for (int i = 0; i < N; ++i) x = x + a;
+            break;
+        case 1:   // v_fma_f64
+            for (int i = 0; i < N; ++i) x = fma(x, 0.999, a);
+            break;
+        case 2:   // v_max_f64
+            for (int i = 0; i < N; ++i) x = fmax(x, a) + 0.0;
+            break;
+        case 3:   // dpp pair + add
+            for (int i = 0; i < N; ++i) x = dpp<0xB1>(x) + a;
+            break;
+        case 4:   // ds_read_b64 indexed by data + add
+            for (int i = 0; i < N; ++i) {
+                const int q = (int)(__double_as_longlong(x) >> 40) & 63;
+                x = x + lds[q];
+            }
+            break;
+        case 5:   // v_add_f32
+            for (int i = 0; i < N; ++i) xf = xf + (float)a;
+            break;
+        case 6:   // group max: 3 x (dpp pair + max)
+            for (int i = 0; i < N; ++i) {
+                x = fmax(x, dpp<0xB1>(x));
+                x = fmax(x, dpp<0x4E>(x));
+                x = fmax(x, dpp<0x141>(x));
+                x = x + a;
+            }
+            break;
+        case 7:   // int chain: bfe + med3 + lshl_add
+            {
+                unsigned u = (unsigned)threadIdx.x;
+                for (int i = 0; i < N; ++i) {
+                    u = __builtin_amdgcn_ubfe(u * 3u + 7u, 3, 14);
+                    u = min(max((int)u, 5), 9000) * 32 + 11;
+                }
+                x = (double)u;
+            }
+            break;
+        case 9:   // alpha step (maxlog), operands in registers
+        case 10:  // alpha step (maxlog), gammas from LDS per step
+            {
+                const double sg = (threadIdx.x & 1) ? 1.0 : -1.0, pg = -sg;
+                double gs = 0.3 * (threadIdx.x & 7), gp = 0.2 * (threadIdx.x & 3);
+                for (int i = 0; i < N; ++i) {
+                    if (mode == 10) {
+                        gs = lds[(i * 8 + (threadIdx.x >> 3)) & 255];
+                        gp = lds[(i * 8 + 1 + (threadIdx.x >> 3)) & 255];
+                    }
+                    const double ap = dpp<0xB1>(x);
+                    const double xs = fma(sg, gs, x), xp = fma(pg, gp, ap);
+                    double a = fmax(xs, xp);
+                    double m = fmax(a, dpp<0xB1>(a));
+                    m = fmax(m, dpp<0x4E>(m));
+                    m = fmax(m, dpp<0x141>(m));
+                    x = a - m;
+                }
+            }
+            break;
+        case 8:   // v_add_f64 pairs interleaved (2 independent chains)
+            {
+                double y = x * 0.5;
+                for (int i = 0; i < N; ++i) {
+                    x = x + a;
+                    y = y + a;
+                }
+                x += y;
+            }
+            break;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * 64 + threadIdx.x] = x + xf;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+int main()
+{
+    double* out;
+    unsigned long long* cyc;
+    hipMalloc(&out, 64 * 64 * sizeof(double));
+    hipMalloc(&cyc, 64 * sizeof(unsigned long long));
+    const char* names[] = {"v_add_f64", "v_fma_f64", "v_max_f64+add0", "dpp64+add_f64", "ds_read_b64(idx)+add",
+                           "v_add_f32", "gmax3(dpp+max)+add", "int bfe+med3+lshl", "2x add_f64 interleaved",
+                           "alpha step maxlog (regs)", "alpha step maxlog (lds g)"};
+    for (int mode = 0; mode < 11; ++mode) {
+        hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);
+        hipDeviceSynchronize();
+        hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);
+        unsigned long long h[64];
+        hipMemcpy(h, cyc, sizeof h, hipMemcpyDeviceToHost);
+        double s = 0;
+        for (int i = 0; i < 64; ++i) s += h[i];
+        printf("%-26s %8.2f cycles per iteration\n", names[mode], s / 64 / N);
+    }
+    return 0;
+}

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libturbo_mi355x.so")
+LIB_PATH = os.environ.get("TD_LIB_PATH") or os.path.join(PKG, "libturbo_mi355x.so")
 
 TD_OK, TD_EINVAL, TD_ENOMEM, TD_EHIP, TD_ENODEV = 0, 1, 2, 3, 4
 TD_ALGO_LOGMAP, TD_ALGO_MAXLOG = 0, 1
@@ -19,7 +19,8 @@ TD_F64, TD_F32 = 0, 1
 EXPORTS = (
     "td_create", "td_destroy", "td_reserve", "td_decode_device", "td_decode_host", "td_siso_host",
     "td_last_error", "td_device_count", "td_abi_version", "td_maxstar_host_f64", "td_maxstar_host_f32",
-    "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read",
+    "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read", "td_debug_set_stamps",
+    "td_debug_stamp_slots",
 )
 
 
@@ -65,6 +66,8 @@ def lib() -> C.CDLL:
     L.td_trellis_tables.argtypes = [P, P, P]
     L.td_qpp_table.argtypes = [I, I, I, P]
     L.td_profile_enable.argtypes = [P, I]
+    L.td_debug_set_stamps.argtypes = [P, P]
+    L.td_debug_stamp_slots.restype = I
     L.td_profile_read.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
     _lib = L
     return L

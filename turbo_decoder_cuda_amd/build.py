@@ -17,7 +17,9 @@ LIB = os.path.join(PKG, "libturbo_mi355x.so")
 COMPAT = os.path.join(PKG, "libturbo_logmap_compat.so")
 
 # -ffp-contract=off: the parity mode reproduces the reference's operation order exactly.
-COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", f"-I{CSRC}"]
+# -fno-honor-nans: the decoder never produces a NaN from finite channel LLRs; without it hipcc
+# canonicalises every DPP-moved operand (an extra v_max_f64 x,x) before each fmax.
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-honor-nans", f"-I{INC}", f"-I{CSRC}"]
 
 
 def _newer(out: str, srcs) -> bool:
@@ -38,6 +40,9 @@ def build(force: bool = False, verbose: bool = False) -> None:
     if force or _newer(LIB, deps):
         extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose else []
         _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-shared", "-o", LIB, *srcs])
+    stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
+    if force or _newer(stamps, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-shared", "-o", stamps, *srcs])
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,

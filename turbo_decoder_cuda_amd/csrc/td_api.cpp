@@ -43,17 +43,68 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 struct td_handle {
     td_params p{};
     td::Trellis tr{};
+    td::LaneTables lane{};
     std::vector<int> pi;
     int* d_pi = nullptr;
+    int* d_pinv = nullptr;
     void* d_lut = nullptr;
+    td::LaneTables* d_lane = nullptr;
     void* d_ws = nullptr;   // decode workspace
     size_t ws_bytes = 0;
     int ws_groups = 0;
     size_t elem = 8;
+    void* stamps = nullptr;     // td_debug_set_stamps
     bool prof = false;          // td_profile_enable
     std::vector<std::array<hipEvent_t, 3>> ev;   // one triple per profiled decode
     size_t nev = 0;
 };
+
+namespace td {
+
+bool build_lane_tables(const Trellis& t, LaneTables& lt)
+{
+    auto A = [](int l) { return (l & 1) ^ (((l >> 1) & 1) * 2) ^ (((l >> 2) & 1) * 7); };
+    auto rotr = [](int s) { return (s >> 1) | ((s & 1) << 2); };
+    const int m[3] = {1, 2, 7};   // DPP partner masks: quad_perm xor1, quad_perm xor2, row_half_mirror
+    for (int ph = 0; ph < 3; ++ph)
+        for (int l = 0; l < 8; ++l) {
+            int s = A(l);
+            for (int r = 0; r < ph; ++r) s = rotr(s);
+            lt.state[ph][l] = s;
+        }
+    for (int ph = 0; ph < 3; ++ph) {
+        const int nx = (ph + 1) % 3;
+        for (int l = 0; l < 8; ++l) {
+            // alpha i -> i+1: this slot computes state j (labeling nx) from its own value (ps)
+            // and the partner slot's (pp), both at labeling ph
+            const int j = lt.state[nx][l], ps = lt.state[ph][l], pp = lt.state[ph][l ^ m[ph]];
+            const int p0 = t.laststat[j][0], p1 = t.laststat[j][1];
+            if (!((ps == p0 && pp == p1) || (ps == p1 && pp == p0))) return false;
+            const int us = ps == p0 ? 0 : 1;
+            // parity sign o and input u select G: (u == 1) == (o == +1) -> P, else Q
+            const int os = t.nextout[ps][2 * us + 1], op = t.nextout[pp][2 * (1 - us) + 1];
+            lt.a_sg[ph][l] = us ? 1 : -1;
+            lt.a_sel[ph][l] = ((us == 1) == (os == 1)) ? 0 : 1;
+            lt.a_pg[ph][l] = us ? -1 : 1;
+            lt.a_psel[ph][l] = (((1 - us) == 1) == (op == 1)) ? 0 : 1;
+            lt.a_j[ph][l] = j;
+            lt.a_swap[ph][l] = us;
+            // beta i+1 -> i: this slot computes state jb (labeling ph) from successors at labeling nx
+            const int jb = lt.state[ph][l], ns = lt.state[nx][l], np = lt.state[nx][l ^ m[ph]];
+            const int n0 = t.nextstat[jb][0], n1 = t.nextstat[jb][1];
+            if (!((ns == n0 && np == n1) || (ns == n1 && np == n0))) return false;
+            const int ub = ns == n0 ? 0 : 1;
+            const int obs = t.nextout[jb][2 * ub + 1], obp = t.nextout[jb][2 * (1 - ub) + 1];
+            lt.b_sg[ph][l] = ub ? 1 : -1;
+            lt.b_sel[ph][l] = ((ub == 1) == (obs == 1)) ? 0 : 1;
+            lt.b_pg[ph][l] = ub ? -1 : 1;
+            lt.b_psel[ph][l] = (((1 - ub) == 1) == (obp == 1)) ? 0 : 1;
+        }
+    }
+    return true;
+}
+
+}  // namespace td
 
 namespace {
 
@@ -63,6 +114,7 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     std::memcpy(dp.nextstat, h->tr.nextstat, sizeof dp.nextstat);
     std::memcpy(dp.laststat, h->tr.laststat, sizeof dp.laststat);
     std::memcpy(dp.nextout, h->tr.nextout, sizeof dp.nextout);
+    dp.lane = h->d_lane;
     dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
     dp.algo = h->p.algo;
 }
@@ -131,8 +183,10 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.ckpt = reinterpret_cast<T*>(ws + c.ckpt);
     dp.llr_out = nullptr;
     dp.pi = h->d_pi;
+    dp.pinv = h->d_pinv;
     dp.bits = d_bits;
     dp.le_dump = static_cast<T*>(d_le);
+    dp.stamps = static_cast<unsigned long long*>(h->stamps);
     dp.K = h->p.K;
     dp.L = h->p.K + td::kMemory;
     dp.nT = (dp.L + td::window_steps() - 1) / td::window_steps();
@@ -188,6 +242,7 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     T* d_la = reinterpret_cast<T*>(take(inA));
     T* d_llr = reinterpret_cast<T*>(take(inA));
     dp.pi = h->d_pi;
+    dp.pinv = h->d_pinv;
     dp.K = L - td::kMemory;
     dp.L = L;
     dp.nT = nT;
@@ -242,7 +297,7 @@ double td_maxstar_host_f64(double x, double y, int algo)
     static bool init = (td::build_lut<double>(lut), true);
     (void)init;
     if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
-    return td::maxstar_lut<double>(x, y, lut);
+    return td::maxstar_lut_host<double>(x, y, lut);
 }
 
 float td_maxstar_host_f32(float x, float y, int algo)
@@ -251,7 +306,7 @@ float td_maxstar_host_f32(float x, float y, int algo)
     static bool init = (td::build_lut<float>(lut), true);
     (void)init;
     if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
-    return td::maxstar_lut<float>(x, y, lut);
+    return td::maxstar_lut_host<float>(x, y, lut);
 }
 
 int td_create(td_handle** out, const td_params* p)
@@ -285,17 +340,25 @@ int td_create(td_handle** out, const td_params* p)
     td_handle* h = new td_handle();
     h->p = *p;
     h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
-    if (!td::build_trellis(13, 15, h->tr)) {   // G_ROW_1 / G_ROW_2, log_map.h:35-36
+    if (!td::build_trellis(13, 15, h->tr) || !td::build_lane_tables(h->tr, h->lane)) {   // G_ROW_1/2, log_map.h:35-36
         delete h;
-        return fail(TD_EINVAL, "td_create: bad generator");
+        return fail(TD_EINVAL, "td_create: trellis does not fit the rotating-label kernel");
     }
     h->pi = std::move(pi);
     if (hipMalloc(&h->d_pi, sizeof(int) * p->K) != hipSuccess ||
-        hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess) {
+        hipMalloc(&h->d_pinv, sizeof(int) * p->K) != hipSuccess ||
+        hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess ||
+        hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess) {
         td_destroy(h);
         return fail(TD_ENOMEM, "td_create: hipMalloc failed");
     }
     hipError_t e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->d_lane, &h->lane, sizeof(td::LaneTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        std::vector<int> inv(p->K);
+        for (int i = 0; i < p->K; ++i) inv[h->pi[i]] = i;
+        e = hipMemcpy(h->d_pinv, inv.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) {
         if (p->precision == TD_F64) {
             td::LutEntry<double> lut[td::kLutSize];
@@ -321,7 +384,9 @@ int td_destroy(td_handle* h)
     (void)hipSetDevice(h->p.device);
     if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->d_pi) (void)hipFree(h->d_pi);
+    if (h->d_pinv) (void)hipFree(h->d_pinv);
     if (h->d_lut) (void)hipFree(h->d_lut);
+    if (h->d_lane) (void)hipFree(h->d_lane);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     delete h;
@@ -372,6 +437,22 @@ int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launch
     if (launches) *launches = n;
     h->nev = 0;
     return TD_OK;
+}
+
+int td_debug_set_stamps(td_handle* h, void* d_buf)
+{
+    if (!h) return fail(TD_EINVAL, "td_debug_set_stamps: null handle");
+    h->stamps = d_buf;
+    return TD_OK;
+}
+
+int td_debug_stamp_slots(void)
+{
+#ifdef TD_STAMPS
+    return 4 * 7;   // [wave][slot]
+#else
+    return 0;
+#endif
 }
 
 int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le)

@@ -9,6 +9,24 @@
 
 namespace td {
 
+// Per-lane trellis constants of the rotating-label scheme (td_kernels.hip header), indexed
+// [phase = step mod 3][slot = lane & 7]; built and verified on the host (build_lane_tables).
+struct LaneTables {
+    int state[3][8];                     // state held by slot l at a step of phase ph
+    // gamma of a transition = sg * G with G = P (sel 0) or Q (sel 1), sg = +1 (u = 1) / -1 (u = 0),
+    // P = (ys + yp) + La/2, Q = (ys - yp) + La/2 (see td_kernels.hip, "gamma")
+    int a_sg[3][8], a_sel[3][8];         // alpha step, self transition
+    int a_pg[3][8], a_psel[3][8];        // alpha step, partner transition
+    int b_sg[3][8], b_sel[3][8];         // beta step, self transition
+    int b_pg[3][8], b_psel[3][8];        // beta step, partner transition
+    int a_j[3][8];                       // state produced by the alpha step of phase ph
+    int a_swap[3][8];                    // 1 if the self transition has input u = 1
+};
+
+// Builds the tables from the trellis; false if the code is not the 8-state shift-register
+// butterfly the labeling assumes (never for 13/15).
+bool build_lane_tables(const Trellis& t, LaneTables& lt);
+
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
 template <typename T>
@@ -17,18 +35,21 @@ struct DecodeParams {
     T* par1;   // [G][L][8] parity 1
     T* sys2;   // [G][L][8] interleaved systematic (decoder 2)
     T* par2;   // [G][L][8] parity 2
-    T* ext12;  // [G][K][8] Le of decoder 1, natural order
+    T* ext12;  // [G][K][8] Le of decoder 1 scattered to interleaved order (= La of decoder 2)
     T* ext21;  // [G][K][8] Le of decoder 2 scattered to natural order (= La of decoder 1)
     T* ckpt;   // [G][nT+1][64] alpha checkpoints
     T* llr_out;                 // bare SISO: [G][L][8]
-    const int* pi;              // [K]
+    const int* pi;              // [K] QPP
+    const int* pinv;            // [K] inverse QPP
     const LutEntry<T>* lut;     // [kLutSize]
     uint8_t* bits;              // decisions (see td_decode_device)
     T* le_dump;                 // nullable
+    unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
     int K, L, nT, G, B, iters, all_iters, algo;
     int nextstat[kStates][2];
     int laststat[kStates][2];
     int nextout[kStates][4];
+    const LaneTables* lane;     // device copy (dynamic per-lane indexing stays out of scratch)
 };
 
 // demultiplex + x0.5 of the stream into the batch-interleaved arrays

@@ -4,20 +4,17 @@
 //    gen_g_matrix/gen_trellis do (ITTC/log_map.cpp:114-169, 247-269, 281-337);
 //  * the QPP permutation (gen_qpp_index, log_map.cpp:616-624);
 //  * the max* bucket table: an exact, branch-free form of E_algorithm's 16-step linear
-//    scan (log_map.cpp:14-18, 779-801).  d = |y - x| is split into 1/16-wide buckets; no
-//    bucket holds more than one threshold (smallest gap 0.08824 > 1/16), so
-//        f(d) = (d >= thr[q]) ? vhi[q] : vlo[q],   q = min(floor(16 d), 71)
-//    reproduces the reference's table value for every double (or float) d >= 0.
+//    scan (log_map.cpp:14-18, 779-801), see build_lut.
 #pragma once
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 namespace td {
 
 constexpr int kStates = 8;
 constexpr int kMemory = 3;        // M_num_reg (log_map.cpp:28)
-constexpr int kLutSize = 72;      // buckets 0..71 (71 = every d >= 71/16)
 constexpr double kInfty = 1e20;   // INFTY (log_map.h:74-76)
 
 // log_map.cpp:14-18
@@ -95,11 +92,52 @@ inline void build_qpp(int K, int f1, int f2, int* pi)
     for (int i = 0; i < K; ++i) pi[i] = (f1 * i + (((f2 * i) % K) * i) % K) % K;
 }
 
+// Bucket geometry of the max* table.  The bucket index comes straight from the bits of
+// d = |y - x|: exponent + top 3 mantissa bits (8 buckets per octave), clamped to [0, 56]:
+//   bucket 0      d < 2^-4 * 1.125 (below the first threshold 0.08824)
+//   buckets 1..55 [2^e (1 + m/8), 2^e (1 + (m+1)/8)),  e = -4..2
+//   bucket 56     d >= 8                                 (f = 0)
+// Every bucket holds at most one threshold (relative threshold gaps >= 1.19 > 1 + 1/8), so
+//   f(d) = (d >= thr[q]) ? vhi[q] : vlo[q]
+// reproduces the reference's linear scan (log_map.cpp:779-801) for every d >= 0.
+constexpr int kLutSize = 57;
+
+template <typename T>
+struct BucketBits;
+template <>
+struct BucketBits<double> {   // bits 17..30 of the high dword: 11 exponent + 3 mantissa bits
+    static constexpr int shift = 17, width = 14, base = (1023 - 4) << 3;
+};
+template <>
+struct BucketBits<float> {    // bits 20..30: 8 exponent + 3 mantissa bits
+    static constexpr int shift = 20, width = 11, base = (127 - 4) << 3;
+};
+
+inline int bucket_of_bits(unsigned hi, int shift, int width, int base)
+{
+    int q = (int)((hi >> shift) & ((1u << width) - 1)) - base;
+    return q < 0 ? 0 : (q > kLutSize - 1 ? kLutSize - 1 : q);
+}
+
+inline unsigned high_word(double d)
+{
+    unsigned long long b;
+    std::memcpy(&b, &d, sizeof b);
+    return (unsigned)(b >> 32);
+}
+inline unsigned high_word(float d)
+{
+    unsigned b;
+    std::memcpy(&b, &d, sizeof b);
+    return b;
+}
+
 // The bucket table for precision T.  Thresholds and values are the reference's doubles
 // rounded once to T (exact for T = double).
 template <typename T>
 inline void build_lut(LutEntry<T>* lut)
 {
+    using BB = BucketBits<T>;
     T thr[16], val[16];
     for (int k = 0; k < 16; ++k) {
         thr[k] = (T)kIdx[k];
@@ -109,9 +147,9 @@ inline void build_lut(LutEntry<T>* lut)
     for (int q = 0; q < kLutSize; ++q) {
         int base = 0, in_bucket = -1;
         for (int k = 1; k < 16; ++k) {
-            double fl = std::floor((double)thr[k] * 16.0);
-            if (fl < q) ++base;
-            if ((int)fl == q) in_bucket = k;
+            const int qk = bucket_of_bits(high_word(thr[k]), BB::shift, BB::width, BB::base);
+            if (qk < q) ++base;
+            if (qk == q) in_bucket = k;
         }
         lut[q].thr = in_bucket >= 0 ? thr[in_bucket] : (T)INFINITY;
         lut[q].vlo = val[base];
@@ -120,43 +158,15 @@ inline void build_lut(LutEntry<T>* lut)
     }
 }
 
-// Bucket max*, host/device.  fabs(y-x) equals the reference's (y-x)>0?(y-x):(x-y) exactly
-// (IEEE negation is exact), and max(x,y) equals x>y?x:y for every non-NaN pair.
+// Host evaluation of the bucket max* (the device form lives in td_kernels.hip).
 template <typename T>
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-inline T bucket_index_clamp(T d);
-
-template <>
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-inline double bucket_index_clamp<double>(double d)
+inline T maxstar_lut_host(T x, T y, const LutEntry<T>* lut)
 {
-    return fmin(d * 16.0, 71.0);
-}
-
-template <>
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-inline float bucket_index_clamp<float>(float d)
-{
-    return fminf(d * 16.0f, 71.0f);
-}
-
-template <typename T>
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-inline T maxstar_lut(T x, T y, const LutEntry<T>* lut)
-{
+    using BB = BucketBits<T>;
     T d = y - x;
     d = d < (T)0 ? -d : d;
-    T m = x > y ? x : y;
-    int q = (int)bucket_index_clamp<T>(d);
-    const LutEntry<T> e = lut[q];
+    const T m = x > y ? x : y;
+    const LutEntry<T>& e = lut[bucket_of_bits(high_word(d), BB::shift, BB::width, BB::base)];
     return m + (d >= e.thr ? e.vhi : e.vlo);
 }
 
