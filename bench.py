@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--ebn0", type=float, default=1.0)
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
-    ap.add_argument("--cpu-sample", type=int, default=256, help="codewords for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="codewords for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-variants", action="store_true")
     return ap.parse_args()
@@ -67,8 +67,9 @@ def load_traffic(cfg_key):
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(cfg_key)
-    except (OSError, ValueError):
+            rec = json.load(f).get(cfg_key)
+        return int(rec["bytes_per_launch"]) if rec else None
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
@@ -87,7 +88,6 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     f1, f2 = qpp_for(a.K)
-    np_dt = np.float64 if a.precision == "f64" else np.float32
     u, llr_h = synth.make_batch(a.batch, a.K, f1, f2, a.ebn0, seed=20261015 + rank, dtype=np.float64)
     llr64 = torch.from_numpy(llr_h).to(dev)
     llr = llr64 if a.precision == "f64" else llr64.float()
@@ -118,28 +118,49 @@ def main():
     demux_ms, turbo_ms, nlaunch = codec.kernel_ms()
     codec.profile(False)
 
-    elapsed = t1 - t0
     errs = int((bits != u_d).sum().item())
     blk = int((bits != u_d).any(dim=1).sum().item())
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        e = torch.tensor([errs, blk], dtype=torch.int64)
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        errs, blk = int(e[0]), int(e[1])
+    elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
+    out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
 
+    if rank == 0 and world == 1 and not a.no_variants:
+        out["pcie_inclusive"] = pcie_inclusive(a, codec, llr, dev, stream)
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(a, llr_h, bits.cpu().numpy(), f1, f2)
+    if rank == 0 and world == 1 and not a.no_variants:
+        out["variants"] = variants(a, llr64, u_d, f1, f2, dev, stream)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def reduce_over_ranks(elapsed: float, errs: int, blk: int, world: int):
+    """Max of the timed-region wall time and sum of the error counters over ranks (gloo, host
+    scalars: the only cross-rank exchange; the decode itself has no collective)."""
+    if world <= 1:
+        return elapsed, errs, blk
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([errs, blk], dtype=torch.int64)
+    dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(e[0]), int(e[1])
+
+
+def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2) -> dict:
+    """The bench JSON record.  value = info bits decoded by ALL ranks / max-over-ranks time."""
     ms_step = elapsed / a.steps * 1e3
     total_bits = world * a.batch * a.K * a.steps
     value = total_bits / elapsed / 1e6
     esz = 8 if a.precision == "f64" else 4
     bytes_cw = esz * (3 * a.K + 12) + a.K   # algorithmic: LLR in + uint8 bits out (SURVEY.md 8d)
     alg_bytes = bytes_cw * a.batch
-    achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9 if turbo_ms > 0 else 0.0
     cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}"
-    traffic = load_traffic(cfg_key)
-
-    out = {
+    return {
         "metric": METRIC,
         "value": round(value, 3),
         "unit": "Mbit/s",
@@ -168,7 +189,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6),
-            "traffic": traffic,
+            "traffic": load_traffic(cfg_key),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_codeword": bytes_cw,
             "kernel_ms_avg": round(turbo_ms, 4),
@@ -178,15 +199,6 @@ def main():
         "ber": {"bit_errors": errs, "block_errors": blk,
                 "ber": errs / (world * a.batch * a.K), "bler": blk / (world * a.batch)},
     }
-
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(a, llr_h, bits.cpu().numpy(), f1, f2)
-    if rank == 0 and world == 1 and not a.no_variants:
-        out["variants"] = variants(a, llr64, u_d, f1, f2, dev, stream)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def cpu_baseline(a, llr_h, gpu_bits, f1, f2):
@@ -214,6 +226,27 @@ def cpu_baseline(a, llr_h, gpu_bits, f1, f2):
         "bits_match_gpu": bool(np.array_equal(cb, gpu_bits[:n])),
         "cpu_model": _cpu_model(),
     }
+
+
+def pcie_inclusive(a, codec, llr, dev, stream):
+    """Host-resident flow: pinned H2D of the LLRs + decode + D2H of the bits, per batch (not the
+    headline value)."""
+    import torch
+
+    h_llr = llr.cpu().pin_memory()
+    h_bits = torch.empty((a.batch, a.K), dtype=torch.uint8).pin_memory()
+    d_bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
+    steps = max(2, a.steps // 2)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        llr.copy_(h_llr, non_blocking=True)
+        codec.decode(llr, d_bits, stream=stream)
+        h_bits.copy_(d_bits, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(a.batch * a.K / dt / 1e6, 3), "unit": "Mbit/s", "ms_per_step": round(dt * 1e3, 4),
+            "note": "pinned H2D of the fp64 LLR batch + decode + D2H of the bits, serial on one stream"}
 
 
 def variants(a, llr64, u_d, f1, f2, dev, stream):

@@ -111,7 +111,7 @@ int td_abi_version(void);
 
 /*
  * Host evaluation of the exact bucket form of E_algorithm used on the device (no GPU needed):
- * max(x,y) + table(|y-x|) through the 72-entry LUT the kernels read from LDS.  Lets CPU
+ * max(x,y) + table(|y-x|) through the 57-bucket LUT the kernels read from LDS.  Lets CPU
  * tests prove LUT == log_map.cpp:779-801 for every threshold.  algo = enum td_algo.
  */
 double td_maxstar_host_f64(double x, double y, int algo);

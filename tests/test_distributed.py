@@ -1,0 +1,56 @@
+"""Multi-rank bench logic on CPU (gloo, world_size 2): each rank decodes its own shard of
+codewords, so the only exchange is the max of the timed-region wall time and the sum of the
+error counters (bench.reduce_over_ranks); value = all ranks' info bits / max time."""
+import argparse
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    elapsed = [2.0, 2.5][rank]
+    errs, blk = [10, 3][rank], [1, 2][rank]
+    e, n, b = bench.reduce_over_ranks(elapsed, errs, blk, world)
+    a = argparse.Namespace(steps=4, warmup=1, batch=64, K=1024, iters=8, ebn0=1.0, precision="f64",
+                           algo="logmap")
+    rec = bench.summarize(a, world, e, n, b, 0.1, 100.0, 4, 31, 64)
+    q.put((rank, e, n, b, rec))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, e, n, b, rec in res:
+        assert (e, n, b) == (2.5, 13, 3)
+        assert rec["n_gpus"] == 2 and rec["scaling"] == "weak"
+        assert rec["value"] == pytest.approx(2 * 64 * 1024 * 4 / 2.5 / 1e6, abs=1e-3)
+        assert rec["config"]["global_batch"] == 128
+        assert rec["ber"]["bit_errors"] == 13
+        assert rec["roofline"]["alg_bytes_per_codeword"] == 8 * (3 * 1024 + 12) + 1024
