@@ -4,7 +4,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["TD_LIB_PATH"] = os.path.join(REPO, "turbo_decoder_cuda_amd", "libturbo_mi355x_stamps.so")
+os.environ["TD_LIB_PATH"] = os.environ.get("TD_STAMPS_LIB") or os.path.join(REPO, "turbo_decoder_cuda_amd",
+                                                                             "libturbo_mi355x_stamps.so")
 sys.path.insert(0, REPO)
 import ctypes as C  # noqa: E402
 
@@ -34,7 +35,16 @@ s = st.cpu().numpy().reshape(G, 4, 7).astype(np.float64)
 L = K + 3
 steps = 2 * iters * L
 print(f"B={B} {prec} {algo} kernel_ms={kms:.3f} errs={int((bits.cpu().numpy() != u).sum())}")
-roles = ["A alpha", "B beta", "F0 fold+load", "F1 fold"]
+roles = ["A alpha|fold", "B beta", "F0 loader", "F1 fold"]
 for w in range(4):
     fw, fwait, bw, bwait = (s[:, w, i].mean() / steps for i in range(4))
-    print(f"  {roles[w]:14s} per SISO-step: F work {fw:7.1f}  F wait {fwait:7.1f}  B work {bw:7.1f}  B wait {bwait:7.1f}")
+    print(f"  {roles[w]:14s} per SISO-step: F work {fw:7.1f}  F wait {fwait:7.1f}  B work {bw:7.1f}  B wait {bwait:7.1f}"
+          f"  (slot4 {s[:, w, 4].mean() / steps:6.1f})")
+hw = st.cpu().numpy().reshape(G, 4, 7)[:, :, 6].astype(np.int64)
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+se = (hw >> 13) & 7
+distinct = np.array([len(set(simd[g])) for g in range(G)])
+print("  waves of a group on distinct SIMDs: " + ", ".join(f"{k}:{int((distinct == k).sum())}" for k in (1, 2, 3, 4)))
+same = lambda a, b: int((simd[:, a] == simd[:, b]).sum())
+print(f"  A/B share SIMD in {same(0, 1)} groups, A/F0 {same(0, 2)}, A/F1 {same(0, 3)}, B/F0 {same(1, 2)}, B/F1 {same(1, 3)}")

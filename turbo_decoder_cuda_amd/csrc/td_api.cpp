@@ -121,17 +121,15 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
 
 // Workspace carve for G groups of the handle's K.
 struct Carve {
-    size_t sys1, par1, sys2, par2, ext12, ext21, ckpt, total;
+    size_t sys1, par1, sys2, par2, ext12, ext21, astore, tmstore, total;
 };
 
 Carve carve(int G, int K, size_t elem)
 {
     const int L = K + td::kMemory;
-    const int W = td::window_steps();
-    const int nT = (L + W - 1) / W;
     const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
     const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
-    const size_t ck = align_up((size_t)G * (nT + 1) * 64 * elem, 256);
+    const size_t arrA = align_up((size_t)G * L * 64 * elem, 256);
     Carve c{};
     c.sys1 = 0;
     c.par1 = c.sys1 + arrL;
@@ -139,8 +137,9 @@ Carve carve(int G, int K, size_t elem)
     c.par2 = c.sys2 + arrL;
     c.ext12 = c.par2 + arrL;
     c.ext21 = c.ext12 + arrK;
-    c.ckpt = c.ext21 + arrK;
-    c.total = c.ckpt + ck;
+    c.astore = c.ext21 + arrK;
+    c.tmstore = c.astore + arrA;
+    c.total = c.tmstore + arrL;
     return c;
 }
 
@@ -180,7 +179,8 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.par2 = reinterpret_cast<T*>(ws + c.par2);
     dp.ext12 = reinterpret_cast<T*>(ws + c.ext12);
     dp.ext21 = reinterpret_cast<T*>(ws + c.ext21);
-    dp.ckpt = reinterpret_cast<T*>(ws + c.ckpt);
+    dp.astore = reinterpret_cast<T*>(ws + c.astore);
+    dp.tmstore = reinterpret_cast<T*>(ws + c.tmstore);
     dp.llr_out = nullptr;
     dp.pi = h->d_pi;
     dp.pinv = h->d_pinv;
@@ -220,10 +220,12 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     const int W = td::window_steps();
     const int nT = (L + W - 1) / W;
     const size_t eL = (size_t)G * L * 8 * sizeof(T);
-    const size_t ck = (size_t)G * (nT + 1) * 64 * sizeof(T);
+    const size_t eA = (size_t)G * L * 64 * sizeof(T);
     const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
     char* buf = nullptr;
-    const size_t total = 4 * align_up(eL, 256) + align_up(ck, 256) + align_up(inR, 256) + 2 * align_up(inA, 256);
+    const size_t eP = (size_t)L * sizeof(int);   // zero permutation tables: the bare SISO writes no extrinsic
+    const size_t total = 5 * align_up(eL, 256) + align_up(eA, 256) + align_up(inR, 256) + 2 * align_up(inA, 256) +
+                         align_up(eP, 256);
     if (hipMalloc(&buf, total) != hipSuccess) return fail(TD_ENOMEM, "hipMalloc (siso) failed");
     size_t o = 0;
     auto take = [&](size_t n) {
@@ -237,12 +239,14 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     dp.par1 = reinterpret_cast<T*>(take(eL));
     T* la_ws = reinterpret_cast<T*>(take(eL));
     dp.llr_out = reinterpret_cast<T*>(take(eL));
-    dp.ckpt = reinterpret_cast<T*>(take(ck));
+    dp.astore = reinterpret_cast<T*>(take(eA));
+    dp.tmstore = reinterpret_cast<T*>(take(eL));
     T* d_recs = reinterpret_cast<T*>(take(inR));
     T* d_la = reinterpret_cast<T*>(take(inA));
     T* d_llr = reinterpret_cast<T*>(take(inA));
-    dp.pi = h->d_pi;
-    dp.pinv = h->d_pinv;
+    int* d_zero_perm = reinterpret_cast<int*>(take(eP));
+    dp.pi = d_zero_perm;
+    dp.pinv = d_zero_perm;
     dp.K = L - td::kMemory;
     dp.L = L;
     dp.nT = nT;
@@ -250,7 +254,8 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     dp.B = B;
     dp.iters = 1;
     int rc = TD_OK;
-    hipError_t e = hipMemcpy(d_recs, recs, inR, hipMemcpyHostToDevice);
+    hipError_t e = hipMemset(d_zero_perm, 0, eP);
+    if (e == hipSuccess) e = hipMemcpy(d_recs, recs, inR, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_la, La, inA, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = td::launch_siso<T>(dp, d_recs, d_la, la_ws, terminated, d_llr, nullptr);
     if (e == hipSuccess) e = hipMemcpy(LLR, d_llr, inA, hipMemcpyDeviceToHost);
@@ -340,7 +345,7 @@ int td_create(td_handle** out, const td_params* p)
     td_handle* h = new td_handle();
     h->p = *p;
     h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
-    if (!td::build_trellis(13, 15, h->tr) || !td::build_lane_tables(h->tr, h->lane)) {   // G_ROW_1/2, log_map.h:35-36
+    if (!td::build_trellis(13, 15, h->tr) || !td::build_lane_tables(h->tr, h->lane) || !td::trellis_is_lte(h->tr)) {   // G_ROW_1/2, log_map.h:35-36
         delete h;
         return fail(TD_EINVAL, "td_create: trellis does not fit the rotating-label kernel");
     }

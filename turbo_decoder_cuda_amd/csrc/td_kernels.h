@@ -37,7 +37,8 @@ struct DecodeParams {
     T* par2;   // [G][L][8] parity 2
     T* ext12;  // [G][K][8] Le of decoder 1 scattered to interleaved order (= La of decoder 2)
     T* ext21;  // [G][K][8] Le of decoder 2 scattered to natural order (= La of decoder 1)
-    T* ckpt;   // [G][nT+1][64] alpha checkpoints
+    T* astore;    // [G][L][64] alpha[.][i] by 8c + state (F pass -> B pass scratch)
+    T* tmstore;   // [G][L][8] tempmax[i+1] per step and codeword
     T* llr_out;                 // bare SISO: [G][L][8]
     const int* pi;              // [K] QPP
     const int* pinv;            // [K] inverse QPP

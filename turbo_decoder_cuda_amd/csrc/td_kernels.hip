@@ -135,57 +135,59 @@ struct LaneConst {
     int a_sel[3], a_psel[3];
     T b_sg[3], b_pg[3];    // beta step i+1 -> i
     int b_sel[3], b_psel[3];
-    int a_offS[3], a_offP[3];   // LDS offsets of the self / partner LLR term: u*(W*64) + 8c + state
-    int bv_off[3];              // LDS offset of beta[.][i+1] for the LLR terms: 8c + state
-    int a_init0;                // alpha[.][0]: this lane holds state 0 at phase 0
-    int b_init0;                // bit PH: this lane holds state 0 at phase PH (beta[.][L])
+    int st_off[3];         // 8c + state held by this lane at phase PH: alpha / beta stored by state
+    int tm_writer;         // one lane per codeword stores tempmax
+    int a_init0;           // alpha[.][0]: this lane holds state 0 at phase 0
+    int b_init0;           // bit PH: this lane holds state 0 at phase PH (beta[.][L])
 };
 
+// (re)loaded per SISO by the two recursion waves only, so the other roles keep no copy live
 template <typename T>
-__device__ __forceinline__ void lane_setup(const DecodeParams<T>& p, int lane, LaneConst<T>& lc)
+__device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneConst<T>& lc)
 {
     const int slot = lane & 7, c8 = lane & ~7;
 #pragma unroll
     for (int ph = 0; ph < 3; ++ph) {
-        lc.a_sg[ph] = (T)p.lane->a_sg[ph][slot];
-        lc.a_pg[ph] = (T)p.lane->a_pg[ph][slot];
-        lc.a_sel[ph] = p.lane->a_sel[ph][slot];
-        lc.a_psel[ph] = p.lane->a_psel[ph][slot];
-        lc.b_sg[ph] = (T)p.lane->b_sg[ph][slot];
-        lc.b_pg[ph] = (T)p.lane->b_pg[ph][slot];
-        lc.b_sel[ph] = p.lane->b_sel[ph][slot];
-        lc.b_psel[ph] = p.lane->b_psel[ph][slot];
-        const int j = p.lane->a_j[ph][slot], sw = p.lane->a_swap[ph][slot];
-        lc.a_offS[ph] = sw * (kW * kLanes) + c8 + j;
-        lc.a_offP[ph] = (1 - sw) * (kW * kLanes) + c8 + j;
-        lc.bv_off[ph] = c8 + j;
+        lc.a_sg[ph] = (T)lt->a_sg[ph][slot];
+        lc.a_pg[ph] = (T)lt->a_pg[ph][slot];
+        lc.a_sel[ph] = lt->a_sel[ph][slot];
+        lc.a_psel[ph] = lt->a_psel[ph][slot];
+        lc.b_sg[ph] = (T)lt->b_sg[ph][slot];
+        lc.b_pg[ph] = (T)lt->b_pg[ph][slot];
+        lc.b_sel[ph] = lt->b_sel[ph][slot];
+        lc.b_psel[ph] = lt->b_psel[ph][slot];
+        lc.st_off[ph] = c8 + lt->state[ph][slot];
     }
-    lc.a_init0 = p.lane->state[0][slot] == 0;
-    lc.b_init0 = (p.lane->state[0][slot] == 0) | ((p.lane->state[1][slot] == 0) << 1) |
-                 ((p.lane->state[2][slot] == 0) << 2);
+    lc.tm_writer = slot == 0;
+    lc.a_init0 = lt->state[0][slot] == 0;
+    lc.b_init0 = (lt->state[0][slot] == 0) | ((lt->state[1][slot] == 0) << 1) |
+                 ((lt->state[2][slot] == 0) << 2);
 }
 
 // ------------------------------------------------------------------ workgroup roles
-// One workgroup = 4 waves = 8 codewords.  A SISO runs as a pipeline over windows of kW steps:
-//   wave 0 (A)  alpha: F pass (forward, checkpoints) then the window-by-window recompute;
-//   wave 1 (B)  beta, one window behind the recompute;
-//   wave 2 (F0) LLR folds of the window beta finished last iteration (first half of the
-//               items) + the tile loader (global -> registers -> (P, Q) in LDS, two windows ahead);
-//   wave 3 (F1) the other half of the folds.
-// The iterations end at a raw s_barrier that waits only for LDS (lgkmcnt), so global loads stay
-// in flight across it.  Chain waves run at s_setprio 2 so folds and loads fill their bubbles.
+// One workgroup = 4 waves = 8 codewords.  A SISO is two passes over windows of kW steps:
+//   F pass   wave 0 (A) runs alpha forward and streams alpha (by state) and tempmax of every
+//            step to HBM scratch; wave 2 (F0) loads the (P, Q) tiles two windows ahead.
+//   B pass   windows last..first, a three-stage pipeline per iteration j (wa = tl - j):
+//            wave 1 (B)   beta over window wa+1 (tempmax from LDS), publishing beta by state;
+//            wave 2 (F0)  tiles of window wa, tempmax of wa, alpha of wa+1: HBM -> LDS, loads
+//                         issued two iterations ahead;
+//            waves 0, 3   LLR folds of window wa+2 (beta finished last iteration), one (step,
+//                         codeword) item per lane, both input bits in the same lane.
+// Only the two recursions are serial chains; nothing else waits on them but the barriers.  The
+// barriers are raw `s_waitcnt lgkmcnt(0); s_barrier`, so prefetched global loads stay in flight.
 constexpr int kWaves = 4;
-constexpr int kFoldWaves = 3;                        // waves 1..3 fold (B has slack beside beta)
-constexpr int kFoldPerWave = kTile / kFoldWaves;     // items (step, codeword) per fold wave per window
-static_assert(kTile % kFoldWaves == 0 && 2 * kFoldPerWave <= kLanes, "one fold item per lane pair");
+constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (A and F1) per window
+static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 
 template <typename T>
 struct Smem {
     T lut[3 * kLutPad];        // max* table: thr[64] | vlo[64] | vhi[64]
-    T G[3][kW][kCw][2];        // (P, Q) per step and codeword, ring by window index mod 3
-    T XY[3][2][kW][kLanes];    // [window mod 3][u] LLR terms (gamma + alpha) by state slot 8c + j
-    T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by state slot (LLR terms of step i)
-    T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword
+    T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
+    int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
+    T Av[2][kW][kLanes];       // [window parity] alpha[.][i] by 8c + state (fold input)
+    T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
+    T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
 };
 
 // raw barrier: waits for this wave's LDS traffic only, so prefetched global loads stay in flight
@@ -228,22 +230,27 @@ __device__ __forceinline__ int window_len(const Geom& gm, int t) { return min(kW
 
 // channel values and a-priori of tile element e = k*8 + c of window t.  Every read is sequential:
 // the interleaver permutations are applied when the extrinsic is WRITTEN (fold), so no load
-// address depends on another load.
+// address depends on another load.  Prefetch loads are unconditional (rows clamped into range)
+// and their values are masked only where they are consumed: a load under a lane-dependent branch
+// makes the compiler drain the whole vector-memory queue at the join.
 template <typename T>
 __device__ __forceinline__ void load_elem(const SisoSrc<T>& src, const Geom& gm, int t, int e, T& ys, T& yp, T& la,
                                           bool want_yp)
 {
     const int k = e >> 3, c = e & 7;
-    const int i = t * kW + k;
-    ys = 0;
-    yp = 0;
-    la = 0;
-    if (i < gm.L) {
-        const size_t off = ((size_t)gm.g * gm.L + i) * kCw + c;
-        ys = src.sys[off];
-        if (want_yp) yp = src.par[off];
-        if (src.la && i < src.la_len) la = src.la[((size_t)gm.g * src.la_len + i) * kCw + c];
-    }
+    const int i = min(t * kW + k, gm.L - 1);
+    const size_t off = ((size_t)gm.g * gm.L + i) * kCw + c;
+    ys = src.sys[off];
+    yp = want_yp ? src.par[off] : (T)0;
+    la = (T)0;
+    if (src.la) la = src.la[((size_t)gm.g * src.la_len + min(i, src.la_len - 1)) * kCw + c];
+}
+
+// a-priori of step i as the reference sees it: zero for the tail steps (:1224-1227, 1245-1248)
+template <typename T>
+__device__ __forceinline__ T la_at(const SisoSrc<T>& src, int i, T raw)
+{
+    return i < src.la_len ? raw : (T)0;
 }
 
 // ---- tile loader (wave F0): element e = lane and e = lane + 64 (< kTile) of a window
@@ -252,59 +259,97 @@ constexpr int kLoadPerLane = (kTile + kLanes - 1) / kLanes;   // 2
 template <typename T>
 struct TileRegs {
     T ys[kLoadPerLane], yp[kLoadPerLane], la[kLoadPerLane];
+    int wperm[kLoadPerLane], wbit[kLoadPerLane];
 };
 
+// all loads unconditional (clamped element), so every loader iteration issues the same count
 template <typename T>
-__device__ __forceinline__ void tile_issue(TileRegs<T>& r, const SisoSrc<T>& src, const Geom& gm, int t, int lane)
+__device__ __forceinline__ void tile_issue(TileRegs<T>& r, const SisoSrc<T>& src, const SisoDst<T>& dst,
+                                           const Geom& gm, int t, int lane)
 {
+    const int* pperm = dst.ext_mode == 3 ? gm.pinv : gm.pi;
 #pragma unroll
     for (int q = 0; q < kLoadPerLane; ++q) {
-        const int e = lane + kLanes * q;
-        if (e < kTile) load_elem(src, gm, t, e, r.ys[q], r.yp[q], r.la[q], true);
+        const int e = min(lane + kLanes * q, kTile - 1);
+        load_elem(src, gm, t, e, r.ys[q], r.yp[q], r.la[q], true);
+        const int ik = min(t * kW + (e >> 3), gm.K - 1);
+        r.wperm[q] = pperm[ik];
+        r.wbit[q] = gm.pi[ik];
     }
 }
 
-// (P, Q) of the four branch metrics (see "gamma") into the LDS ring slot of window t
+// (P, Q) of the four branch metrics (see "gamma"), ys and La for the extrinsic, and the write
+// positions, into the LDS ring slot of window t
 template <typename T>
-__device__ __forceinline__ void tile_store(const TileRegs<T>& r, Smem<T>& sm, int t, int lane)
+__device__ __forceinline__ void tile_store(const TileRegs<T>& r, Smem<T>& sm, const SisoSrc<T>& src, int t, int lane)
 {
     T* g = &sm.G[t % 3][0][0][0];
+    int* w = &sm.Wp[t % 3][0][0][0];
 #pragma unroll
     for (int q = 0; q < kLoadPerLane; ++q) {
         const int e = lane + kLanes * q;
         if (e < kTile) {
-            const T hla = r.la[q] / (T)2;
-            g[2 * e] = (r.ys[q] + r.yp[q]) + hla;
-            g[2 * e + 1] = (r.ys[q] - r.yp[q]) + hla;
+            const T la = la_at(src, t * kW + (e >> 3), r.la[q]);
+            const T hla = la / (T)2;
+            g[4 * e] = (r.ys[q] + r.yp[q]) + hla;
+            g[4 * e + 1] = (r.ys[q] - r.yp[q]) + hla;
+            g[4 * e + 2] = r.ys[q];
+            g[4 * e + 3] = la;
+            w[2 * e] = r.wperm[q];
+            w[2 * e + 1] = r.wbit[q];
         }
     }
 }
 
-// ---- fold inputs (waves F0/F1): one item (k, c) per lane
+// ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
+// Scratch layout: alpha [g][L][64] by 8c + state, tempmax [g][L][8].
 template <typename T>
-struct FoldRegs {
-    T ys, la;
-    int wext;   // extrinsic write position (per ext_mode)
-    int wbit;   // decision write position pi[i]
+struct AlphaRegs {
+    T a[kW];   // alpha[.][t*kW + k] of this lane's (codeword, state) slot
 };
 
 template <typename T>
-__device__ __forceinline__ void fold_issue(FoldRegs<T>& r, const SisoSrc<T>& src, const SisoDst<T>& dst,
-                                           const Geom& gm, int t, int e)
+__device__ __forceinline__ void alpha_issue(AlphaRegs<T>& r, const T* astore, const Geom& gm, int t, int lane)
 {
-    T yp;
-    load_elem(src, gm, t, e, r.ys, yp, r.la, false);
-    const int i = t * kW + (e >> 3);
-    const bool in_k = i < gm.K;
-    r.wext = i;
-    if (dst.ext_mode == 2 && in_k) r.wext = gm.pi[i];
-    if (dst.ext_mode == 3 && in_k) r.wext = gm.pinv[i];
-    r.wbit = (dst.bits && in_k) ? gm.pi[i] : 0;
+    const T* src = astore + (size_t)gm.g * gm.L * kLanes + lane;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) r.a[k] = src[(size_t)min(max(t * kW + k, 0), gm.L - 1) * kLanes];
+}
+
+template <typename T>
+__device__ __forceinline__ void alpha_store(const AlphaRegs<T>& r, Smem<T>& sm, int t, int lane)
+{
+#pragma unroll
+    for (int k = 0; k < kW; ++k) sm.Av[t & 1][k][lane] = r.a[k];   // rows past the window end are never read
+}
+
+template <typename T>
+struct TmRegs {
+    T v[2];    // elements 2*lane, 2*lane+1 of the window's [kW][8] tempmax block (lanes < 48)
+};
+
+template <typename T>
+__device__ __forceinline__ void tm_issue(TmRegs<T>& r, const T* tmstore, const Geom& gm, int t, int lane)
+{
+    const int e = min(max(t * kW * kCw + 2 * lane, 0), gm.L * kCw - 2);   // clamped: always a valid pair
+    const T* src = tmstore + (size_t)gm.g * gm.L * kCw + e;
+    r.v[0] = src[0];
+    r.v[1] = src[1];
+}
+
+template <typename T>
+__device__ __forceinline__ void tm_store(const TmRegs<T>& r, Smem<T>& sm, int t, int lane)
+{
+    const int e = 2 * lane;
+    if (e < kTile) {
+        T* d = &sm.tm[t & 1][0][0] + e;
+        d[0] = r.v[0];
+        d[1] = r.v[1];
+    }
 }
 
 // ---- recursion steps
-// Operands of one step are read from LDS ahead of the step group that uses them (the compiler
-// cannot prove the LLR-term stores do not alias these reads).
+// Operands of one step are read from LDS ahead of the step group that uses them.
 template <typename T>
 struct StepIn {
     T gs, gp;   // gamma magnitudes (P or Q) of the self / partner transition
@@ -326,32 +371,29 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
     return StepIn<T>{g[lc.b_sel[PH]], g[lc.b_psel[PH]], tmw[k * kCw + c]};
 }
 
-// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  STORE: keep the LLR terms
-// (by state and input u) and tempmax of the step for beta and the folds.
-template <typename T, int ALGO, int PH, bool STORE>
+// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  Streams alpha[.][i] (by state)
+// and tempmax[i+1] of the step to HBM scratch (fire and forget: nothing waits on these stores).
+template <typename T, int ALGO, int PH>
 __device__ __forceinline__ T alpha_step(T alpha, const StepIn<T>& in, const T* lut, int k, int c,
-                                        const LaneConst<T>& lc, T* XYw, T* tmw)
+                                        const LaneConst<T>& lc, T* ga, T* gtm)
 {
+    ga[k * kLanes + lc.st_off[PH]] = alpha;
     const T ap = dpp<PhaseDpp<PH>::ctrl>(alpha);
     const T xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
     const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
     const T a = mstar<T, ALGO>(xs, xp, lut);
     const T m = group_max8(a);
-    if constexpr (STORE) {
-        XYw[k * kLanes + lc.a_offS[PH]] = xs;
-        XYw[k * kLanes + lc.a_offP[PH]] = xp;
-        tmw[k * kCw + c] = m;   // the 8 lanes of a codeword hold the same m
-    }
+    if (lc.tm_writer) gtm[k * kCw + c] = m;
     return a - m;
 }
 
-// beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  Publishes beta[.][i+1] for the
-// LLR terms of step i first.
+// beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  Publishes beta[.][i+1] (by
+// state) for the LLR terms of step i first.
 template <typename T, int ALGO, int PH>
 __device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut, int k,
                                        const LaneConst<T>& lc, T* Bvw)
 {
-    Bvw[k * kLanes + lc.bv_off[PH]] = beta;
+    Bvw[k * kLanes + lc.st_off[(PH + 1) % 3]] = beta;
     const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
     const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], in.gs, beta), fma(lc.b_pg[PH], in.gp, bp), lut);
     return b - in.tm;
@@ -366,10 +408,10 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, int
     return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), sm.lut, k, lc, Bvw);
 }
 
-// alpha over the n steps of window t (window starts are = 0 mod 3)
-template <typename T, int ALGO, bool STORE>
+// alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW
+template <typename T, int ALGO>
 __device__ __forceinline__ T alpha_window(T alpha, int t, int n, const Smem<T>& sm, int c, const LaneConst<T>& lc,
-                                          T* XYw, T* tmw)
+                                          T* ga, T* gtm)
 {
     const int tb = t % 3;
     int k = 0;
@@ -377,15 +419,13 @@ __device__ __forceinline__ T alpha_window(T alpha, int t, int n, const Smem<T>& 
         const StepIn<T> i0 = alpha_in<T, 0>(sm, tb, k, c, lc);
         const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
         const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        alpha = alpha_step<T, ALGO, 0, STORE>(alpha, i0, sm.lut, k, c, lc, XYw, tmw);
-        alpha = alpha_step<T, ALGO, 1, STORE>(alpha, i1, sm.lut, k + 1, c, lc, XYw, tmw);
-        alpha = alpha_step<T, ALGO, 2, STORE>(alpha, i2, sm.lut, k + 2, c, lc, XYw, tmw);
+        alpha = alpha_step<T, ALGO, 0>(alpha, i0, sm.lut, k, c, lc, ga, gtm);
+        alpha = alpha_step<T, ALGO, 1>(alpha, i1, sm.lut, k + 1, c, lc, ga, gtm);
+        alpha = alpha_step<T, ALGO, 2>(alpha, i2, sm.lut, k + 2, c, lc, ga, gtm);
     }
-    if (k < n)
-        alpha = alpha_step<T, ALGO, 0, STORE>(alpha, alpha_in<T, 0>(sm, tb, k, c, lc), sm.lut, k, c, lc, XYw, tmw);
+    if (k < n) alpha = alpha_step<T, ALGO, 0>(alpha, alpha_in<T, 0>(sm, tb, k, c, lc), sm.lut, k, c, lc, ga, gtm);
     if (k + 1 < n)
-        alpha = alpha_step<T, ALGO, 1, STORE>(alpha, alpha_in<T, 1>(sm, tb, k + 1, c, lc), sm.lut, k + 1, c, lc, XYw,
-                                              tmw);
+        alpha = alpha_step<T, ALGO, 1>(alpha, alpha_in<T, 1>(sm, tb, k + 1, c, lc), sm.lut, k + 1, c, lc, ga, gtm);
     return alpha;
 }
 
@@ -421,36 +461,47 @@ __device__ __forceinline__ T fold8(const T* v, const T* lut)
     return t;
 }
 
-// LLR fold + extrinsic + outputs of item e = k*8 + c of window t (:1024-1039, :1234-1264), on a
-// lane pair: the odd lane folds temp1 (u = 1), the even lane temp0 (u = 0); the even lane
-// combines LLR = E_seq(temp1) - E_seq(temp0) and writes the outputs.  All lanes of the wave
-// must call this (DPP exchange); `live` masks the lanes whose item is outside the window.
+// LLR fold + extrinsic + outputs of item e = k*8 + c of window t (:1024-1039, :1234-1264):
+//   temp_u[j] = (gamma[p][i][u] + alpha[p][i]) + beta[j][i+1],  p = laststat[j][u],
+//   LLR = E_seq(temp1) - E_seq(temp0)
+// with gamma[p][.][u] = +-P or +-Q (see "gamma"; kTrellisQ) -- the same two roundings as the
+// reference's (gamma + alpha) + beta.  Both folds run in the same lane (independent chains).
 template <typename T, int ALGO>
-__device__ __forceinline__ void fold_item(const Smem<T>& sm, const FoldRegs<T>& fr, int t, int e, bool live,
-                                          const SisoDst<T>& dst, const Geom& gm, int lane)
+__device__ __forceinline__ void fold_item(const Smem<T>& sm, int t, int e, const SisoDst<T>& dst, const Geom& gm)
 {
-    const int k = e >> 3, c = e & 7, u = lane & 1;
-    const int xs = t % 3, bs = t & 1;
+    const int k = e >> 3, c = e & 7;
     const int i = t * kW + k;
-    T r = (T)0;
-    if (live) {
-        T tv[8];
+    const T* g = &sm.G[t % 3][k][c][0];
+    const T P = g[0], Q = g[1], ys = g[2], la = g[3];
+    const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
+    const T* av = &sm.Av[t & 1][k][c * 8];
+    const T* bv = &sm.Bv[t & 1][k][c * 8];
+    T a[8], b[8], t0[8], t1[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)   // temp_u[j] = (gamma + alpha) + beta[j][i+1]
-            tv[j] = sm.XY[xs][u][k][c * 8 + j] + sm.Bv[bs][k][c * 8 + j];
-        r = fold8<T, ALGO>(tv, sm.lut);
+    for (int j = 0; j < 8; ++j) {
+        a[j] = av[j];
+        b[j] = bv[j];
     }
-    const T r1 = dpp<kDppXor1>(r);   // the odd partner's E_seq(temp1)
-    if (!live || u) return;
-    const T llr = r1 - r;
-    const T le = llr - fr.la - (T)2 * fr.ys;
-    const int b = gm.g * kCw + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
+        t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
+    }
+    const T r0 = fold8<T, ALGO>(t0, sm.lut);
+    const T r1 = fold8<T, ALGO>(t1, sm.lut);
+    const T llr = r1 - r0;
+    const T le = llr - la - (T)2 * ys;
+    const int b_ = gm.g * kCw + c;
     if (dst.llr) dst.llr[((size_t)gm.g * gm.L + i) * kCw + c] = llr;
-    if (dst.ext_mode && i < dst.ext_len) dst.ext[((size_t)gm.g * dst.ext_len + fr.wext) * kCw + c] = le;
-    if (b < gm.B) {
-        if (dst.le_dump) dst.le_dump[(size_t)b * dst.dump_stride + (size_t)dst.dump_slot * gm.L + i] = le;
+    if (dst.ext_mode && i < dst.ext_len) {
+        const int w = dst.ext_mode == 1 ? i : wperm;
+        dst.ext[((size_t)gm.g * dst.ext_len + w) * kCw + c] = le;
+    }
+    if (b_ < gm.B) {
+        if (dst.le_dump) dst.le_dump[(size_t)b_ * dst.dump_stride + (size_t)dst.dump_slot * gm.L + i] = le;
         if (dst.bits && i < gm.K)   // decision (:862-879: LLR < 0 -> 0, else 1) at pi[i] (:1264)
-            dst.bits[(size_t)b * dst.bits_stride + (size_t)dst.bits_row * gm.K + fr.wbit] = (llr < (T)0) ? 0 : 1;
+            dst.bits[(size_t)b_ * dst.bits_stride + (size_t)dst.bits_row * gm.K + wbit] = (llr < (T)0) ? 0 : 1;
     }
 }
 
@@ -464,82 +515,80 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const FoldRegs<T>& 
 #endif
 constexpr int kStampSlots = 7;   // per wave: F pass, F wait, B work, B wait, -, -, HW_ID (see diag)
 
-// Register sets for data in flight are indexed by window parity through explicit branches and
-// always consumed before they are re-issued: selecting or copying a register whose load is still
-// in flight would force a vmcnt wait (or push the set to scratch).
-
-// loader step: store tile `ws` (< 0: none) from its parity set, then re-issue that parity set
-// with tile `wi` (< 0: none).  When both are given they have the same parity.
-template <typename T>
-__device__ __forceinline__ void loader_step(TileRegs<T>& even, TileRegs<T>& odd, Smem<T>& sm, const SisoSrc<T>& src,
-                                            const Geom& gm, int ws, int wi, int lane)
-{
-    const int par = (ws >= 0 ? ws : wi) & 1;
-    if (par) {
-        if (ws >= 0) tile_store(odd, sm, ws, lane);
-        if (wi >= 0) tile_issue(odd, src, gm, wi, lane);
-    } else {
-        if (ws >= 0) tile_store(even, sm, ws, lane);
-        if (wi >= 0) tile_issue(even, src, gm, wi, lane);
-    }
-}
+// The loader wave keeps one register set per stream, issued one iteration ahead and consumed
+// (stored to LDS) at the start of the next iteration before it is re-issued; it issues the same
+// loads in every iteration (clamped addresses), so the compiler's vmcnt bookkeeping stays exact.
+// The other waves issue no global loads inside the passes (the folds only store).
 
 // One SISO over the workgroup's 8 codewords.  Each role runs its own loops (so only that role's
 // state is live in its code); every role executes the same sequence of wg_sync_lds barriers:
 // 1 (F prologue) + nT (F iterations) + nT + 2 (B iterations).
 template <typename T, int ALGO>
-__device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& dst, const Geom& gm, T* ckpt,
-                        const LaneConst<T>& lc, int wave, int lane, unsigned long long* st)
+__device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& dst, const Geom& gm, T* astore,
+                        T* tmstore, const LaneTables* lt, int wave, int lane, unsigned long long* st)
 {
     (void)st;
     const int nT = gm.nT;
     const int tl = nT - 1;
     const int nB = nT + 2;   // B-pass iterations: j = 0 .. nT+1 (wa = tl - j, wb = wa + 1, wf = wa + 2)
+    T* ga0 = astore + (size_t)gm.g * gm.L * kLanes;
+    T* gtm0 = tmstore + (size_t)gm.g * gm.L * kCw;
 
+    // ===================================== F pass
     if (wave == 0) {
-        // ===================================== A: alpha
         const int c = lane >> 3;
-        T* my_ckpt = ckpt + (size_t)gm.g * (nT + 1) * kLanes + lane;
+        LaneConst<T> lc;
+        lane_setup(lt, lane, lc);
         T alpha = lc.a_init0 ? (T)0 : (T)-kInfty;   // :943,948
+        __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
-        for (int t = 0; t < nT; ++t) {   // F pass: window t, checkpoint at its start
+        for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            my_ckpt[(size_t)t * kLanes] = alpha;
-            alpha = alpha_window<T, ALGO, false>(alpha, t, window_len(gm, t), sm, c, lc, nullptr, nullptr);
+            alpha = alpha_window<T, ALGO>(alpha, t, window_len(gm, t), sm, c, lc, ga0 + (size_t)t * kW * kLanes,
+                                          gtm0 + (size_t)t * kW * kCw);
+            if (t == tl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
             TD_ACC(0, f0, f1);
             TD_ACC(1, f1, f2);
         }
-        // B pass: recompute window wa from its checkpoint (prefetched two windows ahead)
-        T ck_even = (T)0, ck_odd = (T)0;
-        {
-            const T c0 = my_ckpt[(size_t)tl * kLanes];
-            const T c1 = tl > 0 ? my_ckpt[(size_t)(tl - 1) * kLanes] : (T)0;
-            if (tl & 1) {
-                ck_odd = c0;
-                ck_even = c1;
-            } else {
-                ck_even = c0;
-                ck_odd = c1;
-            }
+        __builtin_amdgcn_s_setprio(0);   // in the B pass the beta wave goes first
+    } else if (wave == 2) {
+        // loader: tile t+1 stored at iteration t (issued at t-1), then tile t+2 issued
+        TileRegs<T> tr;
+        tile_issue(tr, src, dst, gm, 0, lane);
+        tile_store(tr, sm, src, 0, lane);
+        tile_issue(tr, src, dst, gm, min(1, tl), lane);
+        wg_sync_lds();
+        for (int t = 0; t < nT; ++t) {
+            TD_STAMP(f0);
+            if (t + 1 <= tl) tile_store(tr, sm, src, t + 1, lane);
+            tile_issue(tr, src, dst, gm, min(t + 2, tl), lane);
+            TD_STAMP(f1);
+            wg_sync_lds();
+            TD_STAMP(f2);
+            TD_ACC(0, f0, f1);
+            TD_ACC(1, f1, f2);
         }
+        // B pass: iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring),
+        // tempmax of wa (beta, next iteration) and alpha of wa+1 (folds, next iteration), each into
+        // the LDS slot nobody reads this iteration, then issues the same streams one window lower.
+        // (The F loop's last issue -- tile tl, unused -- is still in flight and drains here.)
+        AlphaRegs<T> ar;
+        TmRegs<T> mr;
+        tm_issue(mr, tmstore, gm, tl, lane);
+        alpha_issue(ar, astore, gm, tl + 1, lane);   // clamped, unused: keeps the per-iteration pattern
+        tile_issue(tr, src, dst, gm, max(tl - 3, 0), lane);
         for (int j = 0; j < nB; ++j) {
             TD_STAMP(b0);
-            const int wa = tl - j;
-            if (wa >= 0) {
-                T a0;
-                if (wa & 1) {
-                    a0 = ck_odd;
-                    if (wa >= 2) ck_odd = my_ckpt[(size_t)(wa - 2) * kLanes];
-                } else {
-                    a0 = ck_even;
-                    if (wa >= 2) ck_even = my_ckpt[(size_t)(wa - 2) * kLanes];
-                }
-                alpha_window<T, ALGO, true>(a0, wa, window_len(gm, wa), sm, c, lc, &sm.XY[wa % 3][0][0][0],
-                                            &sm.tm[wa & 1][0][0]);
-            }
+            const int wa = tl - j, wb = wa + 1;
+            if (wa >= 0 && wa <= tl - 3) tile_store(tr, sm, src, wa, lane);
+            if (wa >= 0) tm_store(mr, sm, wa, lane);
+            if (wb >= 0 && wb <= tl) alpha_store(ar, sm, wb, lane);
+            tile_issue(tr, src, dst, gm, max(min(wa - 1, tl - 3), 0), lane);
+            tm_issue(mr, tmstore, gm, wa - 1, lane);
+            alpha_issue(ar, astore, gm, wa, lane);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -547,73 +596,49 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             TD_ACC(3, b1, b2);
         }
         return;
+    } else {
+        wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
+        for (int t = 0; t < nT; ++t) {
+            TD_STAMP(f0);
+            TD_STAMP(f1);
+            wg_sync_lds();
+            TD_STAMP(f2);
+            TD_ACC(0, f0, f1);
+            TD_ACC(1, f1, f2);
+        }
     }
 
-    // ===================================== waves 1..3
-    // F pass: wave 2 loads tiles (tile t+1, issued at t-2, into ring slot (t+1) % 3; then issue
-    // tile t+3); waves 1 and 3 only keep the barrier count.
-    TileRegs<T> t_even, t_odd;   // wave 2: tiles in flight by window parity
-    if (wave == 2) {
-        tile_issue(t_even, src, gm, 0, lane);
-        tile_store(t_even, sm, 0, lane);
-        if (nT > 1) tile_issue(t_odd, src, gm, 1, lane);
-        if (nT > 2) tile_issue(t_even, src, gm, 2, lane);
-    }
-    wg_sync_lds();
-    for (int t = 0; t < nT; ++t) {
-        TD_STAMP(f0);
-        if (wave == 2 && t + 1 < nT) loader_step(t_even, t_odd, sm, src, gm, t + 1, t + 3 < nT ? t + 3 : -1, lane);
-        TD_STAMP(f1);
-        wg_sync_lds();
-        TD_STAMP(f2);
-        TD_ACC(0, f0, f1);
-        TD_ACC(1, f1, f2);
-    }
-
-    // B pass: wave 1 runs beta over wb; wave 2 stores tile wa-1 (issued at j-2 as "wa-3"; tiles
-    // tl-2..tl never left the ring) into the slot nobody reads this iteration; waves 1..3 fold
-    // window wf, one item per lane, with inputs prefetched two windows ahead.
-    const int fe = (wave - 1) * kFoldPerWave + (lane >> 1);   // item of this lane pair
-    const bool folder = (lane >> 1) < kFoldPerWave;
-    FoldRegs<T> f_even{}, f_odd{};
-    T beta = (T)0;
+    // ===================================== B pass (waves 0, 1, 3)
     if (wave == 1) {
+        // beta over window wb = tl - j + 1 (its tempmax was staged last iteration)
+        LaneConst<T> lc;
+        lane_setup(lt, lane, lc);
         const int phL = gm.L % 3;   // beta[.][L] lives in the labeling of phase L mod 3
-        beta = (src.terminated && !((lc.b_init0 >> phL) & 1)) ? (T)-kInfty : (T)0;   // :944,951-959
-    }
-    if (folder) {
-        if (tl & 1) {
-            fold_issue(f_odd, src, dst, gm, tl, fe);
-            if (tl > 0) fold_issue(f_even, src, dst, gm, tl - 1, fe);
-        } else {
-            fold_issue(f_even, src, dst, gm, tl, fe);
-            if (tl > 0) fold_issue(f_odd, src, dst, gm, tl - 1, fe);
+        T beta = (src.terminated && !((lc.b_init0 >> phL) & 1)) ? (T)-kInfty : (T)0;   // :944,951-959
+        for (int j = 0; j < nB; ++j) {
+            TD_STAMP(b0);
+            const int wb = tl - j + 1;
+            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lane >> 3, lc);
+            TD_STAMP(b1);
+            wg_sync_lds();
+            TD_STAMP(b2);
+            TD_ACC(2, b0, b1);
+            TD_ACC(3, b1, b2);
         }
-    }
-    for (int j = 0; j < nB; ++j) {
-        TD_STAMP(b0);
-        const int wa = tl - j, wb = wa + 1, wf = wa + 2;
-        if (wave == 1 && wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lane >> 3, lc);
-        if (wave == 2) {
-            const int ws = (wa - 1 >= 0 && wa - 1 <= tl - 3) ? wa - 1 : -1;   // issued at j-2 as "wa-3"
-            const int wi = (wa - 3 >= 0 && wa - 3 <= tl - 3) ? wa - 3 : -1;
-            if (ws >= 0 || wi >= 0) loader_step(t_even, t_odd, sm, src, gm, ws, wi, lane);
+    } else {
+        // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
+        const int fe = (wave == 0 ? 0 : kFoldPerWave) + lane;
+        for (int j = 0; j < nB; ++j) {
+            TD_STAMP(b0);
+            const int wf = tl - j + 2;
+            if (lane < kFoldPerWave && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
+                fold_item<T, ALGO>(sm, wf, fe, dst, gm);
+            TD_STAMP(b1);
+            wg_sync_lds();
+            TD_STAMP(b2);
+            TD_ACC(2, b0, b1);
+            TD_ACC(3, b1, b2);
         }
-        if (wf >= 0 && wf <= tl) {
-            const bool live = folder && (fe >> 3) < window_len(gm, wf);
-            if (wf & 1) {
-                fold_item<T, ALGO>(sm, f_odd, wf, fe, live, dst, gm, lane);
-                if (folder && wf - 2 >= 0) fold_issue(f_odd, src, dst, gm, wf - 2, fe);
-            } else {
-                fold_item<T, ALGO>(sm, f_even, wf, fe, live, dst, gm, lane);
-                if (folder && wf - 2 >= 0) fold_issue(f_even, src, dst, gm, wf - 2, fe);
-            }
-        }
-        TD_STAMP(b1);
-        wg_sync_lds();
-        TD_STAMP(b2);
-        TD_ACC(2, b0, b1);
-        TD_ACC(3, b1, b2);
     }
 }
 
@@ -641,10 +666,8 @@ __global__ __launch_bounds__(256, 2) void turbo_decode_kernel(DecodeParams<T> p)
 {
     Smem<T>& sm = smem<T>();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    LaneConst<T> lc;
-    lane_setup(p, lane, lc);
     lut_to_lds(p, sm, threadIdx.x);
-    if (wave < 2) __builtin_amdgcn_s_setprio(2);   // the recursions first; folds and loads fill in
+    if (wave == 1) __builtin_amdgcn_s_setprio(2);   // beta first; alpha raises itself in the F pass
     __syncthreads();
 
     Geom gm{p.K, p.L, p.nT, p.B, (int)blockIdx.x, p.pi, p.pinv};
@@ -663,7 +686,7 @@ __global__ __launch_bounds__(256, 2) void turbo_decode_kernel(DecodeParams<T> p)
         SisoDst<T> dst{dec ? p.ext21 : p.ext12, dec ? 2 : 3, p.K, nullptr, p.le_dump,
                        want_bits ? p.bits : nullptr, p.all_iters ? it : 0, p.all_iters ? p.iters * p.K : p.K,
                        s, p.iters * 2 * p.L};
-        siso_wg<T, ALGO>(sm, src, dst, gm, p.ckpt, lc, wave, lane, st);
+        siso_wg<T, ALGO>(sm, src, dst, gm, p.astore, p.tmstore, p.lane, wave, lane, st);
         __syncthreads();   // extrinsic stores of this SISO visible to the next one's loads
     }
 #ifdef TD_STAMPS
@@ -680,15 +703,13 @@ __global__ __launch_bounds__(256, 2) void siso_kernel(DecodeParams<T> p, const T
 {
     Smem<T>& sm = smem<T>();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    LaneConst<T> lc;
-    lane_setup(p, lane, lc);
     lut_to_lds(p, sm, threadIdx.x);
-    if (wave < 2) __builtin_amdgcn_s_setprio(2);
+    if (wave == 1) __builtin_amdgcn_s_setprio(2);
     __syncthreads();
     Geom gm{p.K, p.L, p.nT, p.B, (int)blockIdx.x, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, terminated};
     SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0};
-    siso_wg<T, ALGO>(sm, s, d, gm, p.ckpt, lc, wave, lane, nullptr);
+    siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
 }
 
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the

@@ -36,6 +36,12 @@ struct Trellis {
     int laststat[kStates][2];
 };
 
+// The LTE trellis (13/15 octal, G_ROW_1/2 of log_map.h:35-36) as compile-time tables for the
+// LLR fold: laststat[next][u] and "the parity output of a transition out of p makes its branch
+// metric +-Q" (p in {2,3,4,5}; +-P otherwise).  td_create checks build_trellis(13, 15) against them.
+constexpr int kTrellisLast[kStates][2] = {{0, 1}, {3, 2}, {4, 5}, {7, 6}, {1, 0}, {2, 3}, {5, 4}, {6, 7}};
+constexpr int kTrellisQ[kStates] = {0, 0, 1, 1, 1, 1, 0, 0};
+
 // gen_g_matrix (log_map.cpp:114-169): octal -> 4 binary taps, MSB first. false on a non-octal digit.
 inline bool octal_taps(int g, int* taps)
 {
@@ -82,6 +88,20 @@ inline bool build_trellis(int g_fb_oct, int g_ff_oct, Trellis& t)
             t.laststat[ns][u] = s;
             t.lastout[ns][2 * u] = t.nextout[s][2 * u];
             t.lastout[ns][2 * u + 1] = t.nextout[s][2 * u + 1];
+        }
+    return true;
+}
+
+// true when t is the trellis the kernels' compile-time tables describe
+inline bool trellis_is_lte(const Trellis& t)
+{
+    for (int j = 0; j < kStates; ++j)
+        for (int u = 0; u < 2; ++u) {
+            const int p = kTrellisLast[j][u];
+            if (t.laststat[j][u] != p) return false;
+            // u == 1 with parity +1, or u == 0 with parity -1: +-P; otherwise +-Q (see td_kernels.hip "gamma")
+            const int o = t.nextout[p][2 * u + 1];
+            if ((((u == 1) == (o == 1)) ? 0 : 1) != kTrellisQ[p]) return false;
         }
     return true;
 }
