@@ -201,8 +201,9 @@ template <typename T>
 struct SisoSrc {
     const T* sys;
     const T* par;
-    const T* la;      // a-priori la[g][i][c] (i < la_len), already in this decoder's order; null = zeros
-    int la_len;
+    const T* la;      // a-priori la[g][i][c], i < la_cap, already in this decoder's order (always valid memory)
+    int la_cap;       // rows of the la array
+    int la_len;       // steps with a non-zero a-priori (0 = none: the first SISO of the first iteration)
     int terminated;
 };
 
@@ -242,8 +243,7 @@ __device__ __forceinline__ void load_elem(const SisoSrc<T>& src, const Geom& gm,
     const size_t off = ((size_t)gm.g * gm.L + i) * kCw + c;
     ys = src.sys[off];
     yp = want_yp ? src.par[off] : (T)0;
-    la = (T)0;
-    if (src.la) la = src.la[((size_t)gm.g * src.la_len + min(i, src.la_len - 1)) * kCw + c];
+    la = src.la[((size_t)gm.g * src.la_cap + min(i, src.la_cap - 1)) * kCw + c];   // masked at use (la_at)
 }
 
 // a-priori of step i as the reference sees it: zero for the tail steps (:1224-1227, 1245-1248)
@@ -371,19 +371,32 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
     return StepIn<T>{g[lc.b_sel[PH]], g[lc.b_psel[PH]], tmw[k * kCw + c]};
 }
 
-// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  Streams alpha[.][i] (by state)
-// and tempmax[i+1] of the step to HBM scratch (fire and forget: nothing waits on these stores).
+// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  Streams alpha[.][i] (by state,
+// to `pa`) and the previous step's tempmax (`m_prev`, to `ptm`) to HBM scratch.  The stores are
+// issued while the max* table read is in flight, so they cost the chain nothing; nothing ever
+// waits on them inside the pass.
 template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T alpha_step(T alpha, const StepIn<T>& in, const T* lut, int k, int c,
-                                        const LaneConst<T>& lc, T* ga, T* gtm)
+__device__ __forceinline__ T alpha_step(T alpha, T& m_prev, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc,
+                                        T* pa, T* ptm)
 {
-    ga[k * kLanes + lc.st_off[PH]] = alpha;
     const T ap = dpp<PhaseDpp<PH>::ctrl>(alpha);
     const T xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
     const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
-    const T a = mstar<T, ALGO>(xs, xp, lut);
+    T a;
+    if constexpr (ALGO == 1) {
+        *pa = alpha;
+        *ptm = m_prev;
+        a = vmax(xs, xp);
+    } else {
+        const T d = xp - xs;
+        const int q = bucket_dev<T>(d);
+        const T thr = lut[q], lo = lut[kLutPad + q], hi = lut[2 * kLutPad + q];
+        *pa = alpha;
+        *ptm = m_prev;
+        a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
+    }
     const T m = group_max8(a);
-    if (lc.tm_writer) gtm[k * kCw + c] = m;
+    m_prev = m;
     return a - m;
 }
 
@@ -408,24 +421,39 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, int
     return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), sm.lut, k, lc, Bvw);
 }
 
-// alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW
+// alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW.
+// tempmax of step k is stored during step k+1 (index k-1 relative to the step being run); the
+// caller stores the last one.  At t = 0 the first (meaningless) store lands on index 0, which
+// step 1 then overwrites.
 template <typename T, int ALGO>
-__device__ __forceinline__ T alpha_window(T alpha, int t, int n, const Smem<T>& sm, int c, const LaneConst<T>& lc,
-                                          T* ga, T* gtm)
+__device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, const Smem<T>& sm, int c,
+                                          const LaneConst<T>& lc, T* ga, T* gtm)
 {
     const int tb = t % 3;
+    T* pa0 = ga + lc.st_off[0];
+    T* pa1 = ga + kLanes + lc.st_off[1];
+    T* pa2 = ga + 2 * kLanes + lc.st_off[2];
+    T* ptm = gtm + c - (t > 0 ? kCw : 0);
     int k = 0;
     for (; k + 3 <= n; k += 3) {
         const StepIn<T> i0 = alpha_in<T, 0>(sm, tb, k, c, lc);
         const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
         const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        alpha = alpha_step<T, ALGO, 0>(alpha, i0, sm.lut, k, c, lc, ga, gtm);
-        alpha = alpha_step<T, ALGO, 1>(alpha, i1, sm.lut, k + 1, c, lc, ga, gtm);
-        alpha = alpha_step<T, ALGO, 2>(alpha, i2, sm.lut, k + 2, c, lc, ga, gtm);
+        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, i0, sm.lut, lc, pa0 + k * kLanes, ptm);
+        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, i1, sm.lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+        alpha = alpha_step<T, ALGO, 2>(alpha, m_prev, i2, sm.lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+        ptm = gtm + c + (k + 2) * kCw;
     }
-    if (k < n) alpha = alpha_step<T, ALGO, 0>(alpha, alpha_in<T, 0>(sm, tb, k, c, lc), sm.lut, k, c, lc, ga, gtm);
-    if (k + 1 < n)
-        alpha = alpha_step<T, ALGO, 1>(alpha, alpha_in<T, 1>(sm, tb, k + 1, c, lc), sm.lut, k + 1, c, lc, ga, gtm);
+    if (k < n) {
+        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), sm.lut, lc, pa0 + k * kLanes,
+                                       ptm);
+        ptm = gtm + c + k * kCw;
+    }
+    if (k + 1 < n) {
+        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), sm.lut, lc,
+                                       pa1 + k * kLanes, ptm);
+        ptm = gtm + c + (k + 1) * kCw;
+    }
     return alpha;
 }
 
@@ -540,13 +568,17 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
         T alpha = lc.a_init0 ? (T)0 : (T)-kInfty;   // :943,948
+        T m_prev = (T)0;
         __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            alpha = alpha_window<T, ALGO>(alpha, t, window_len(gm, t), sm, c, lc, ga0 + (size_t)t * kW * kLanes,
-                                          gtm0 + (size_t)t * kW * kCw);
-            if (t == tl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
+            alpha = alpha_window<T, ALGO>(alpha, m_prev, t, window_len(gm, t), sm, c, lc,
+                                          ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
+            if (t == tl) {
+                gtm0[(size_t)(gm.L - 1) * kCw + c] = m_prev;   // tempmax[L]
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
+            }
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
@@ -555,45 +587,56 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         __builtin_amdgcn_s_setprio(0);   // in the B pass the beta wave goes first
     } else if (wave == 2) {
-        // loader: tile t+1 stored at iteration t (issued at t-1), then tile t+2 issued
-        TileRegs<T> tr;
-        tile_issue(tr, src, dst, gm, 0, lane);
-        tile_store(tr, sm, src, 0, lane);
-        tile_issue(tr, src, dst, gm, min(1, tl), lane);
-        wg_sync_lds();
-        for (int t = 0; t < nT; ++t) {
+        // loader, two register sets by window parity, two windows ahead; the loops are unrolled by
+        // two so every set is static: F pass iteration t stores tile t+1 and issues tile t+3.
+        TileRegs<T> ts0, ts1;
+        auto fstep = [&](int t, TileRegs<T>& set) {
             TD_STAMP(f0);
-            if (t + 1 <= tl) tile_store(tr, sm, src, t + 1, lane);
-            tile_issue(tr, src, dst, gm, min(t + 2, tl), lane);
+            if (t + 1 <= tl) tile_store(set, sm, src, t + 1, lane);
+            tile_issue(set, src, dst, gm, min(t + 3, tl), lane);
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
             TD_ACC(0, f0, f1);
             TD_ACC(1, f1, f2);
+        };
+        tile_issue(ts0, src, dst, gm, 0, lane);
+        tile_store(ts0, sm, src, 0, lane);
+        tile_issue(ts1, src, dst, gm, min(1, tl), lane);
+        tile_issue(ts0, src, dst, gm, min(2, tl), lane);
+        wg_sync_lds();
+        for (int t = 0; t < nT; t += 2) {
+            fstep(t, ts1);
+            if (t + 1 < nT) fstep(t + 1, ts0);
         }
-        // B pass: iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring),
+        // B pass iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring),
         // tempmax of wa (beta, next iteration) and alpha of wa+1 (folds, next iteration), each into
-        // the LDS slot nobody reads this iteration, then issues the same streams one window lower.
-        // (The F loop's last issue -- tile tl, unused -- is still in flight and drains here.)
-        AlphaRegs<T> ar;
-        TmRegs<T> mr;
-        tm_issue(mr, tmstore, gm, tl, lane);
-        alpha_issue(ar, astore, gm, tl + 1, lane);   // clamped, unused: keeps the per-iteration pattern
-        tile_issue(tr, src, dst, gm, max(tl - 3, 0), lane);
-        for (int j = 0; j < nB; ++j) {
+        // the LDS slot nobody reads this iteration, then issues the same streams two windows lower.
+        AlphaRegs<T> ar;   // alpha: one set, one window ahead (24 VGPRs per set)
+        TmRegs<T> ms0, ms1;
+        auto bstep = [&](int j, TileRegs<T>& ts, TmRegs<T>& ms) {
             TD_STAMP(b0);
             const int wa = tl - j, wb = wa + 1;
-            if (wa >= 0 && wa <= tl - 3) tile_store(tr, sm, src, wa, lane);
-            if (wa >= 0) tm_store(mr, sm, wa, lane);
+            if (wa >= 0 && wa <= tl - 3) tile_store(ts, sm, src, wa, lane);
+            if (wa >= 0) tm_store(ms, sm, wa, lane);
             if (wb >= 0 && wb <= tl) alpha_store(ar, sm, wb, lane);
-            tile_issue(tr, src, dst, gm, max(min(wa - 1, tl - 3), 0), lane);
-            tm_issue(mr, tmstore, gm, wa - 1, lane);
-            alpha_issue(ar, astore, gm, wa, lane);
+            alpha_issue(ar, astore, gm, wb - 1, lane);
+            tile_issue(ts, src, dst, gm, max(min(wa - 2, tl - 3), 0), lane);
+            tm_issue(ms, tmstore, gm, wa - 2, lane);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
             TD_ACC(2, b0, b1);
             TD_ACC(3, b1, b2);
+        };
+        alpha_issue(ar, astore, gm, tl + 1, lane);             // clamped, never stored
+        tile_issue(ts0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never stored
+        tm_issue(ms0, tmstore, gm, tl, lane);
+        tile_issue(ts1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never stored
+        tm_issue(ms1, tmstore, gm, tl - 1, lane);
+        for (int j = 0; j < nB; j += 2) {
+            bstep(j, ts0, ms0);
+            if (j + 1 < nB) bstep(j + 1, ts1, ms1);
         }
         return;
     } else {
@@ -681,8 +724,8 @@ __global__ __launch_bounds__(256, 2) void turbo_decode_kernel(DecodeParams<T> p)
         //            i.e. already as decoder 2's La (:1242).
         // decoder 2: La read in order; its Le is written deinterleaved (ext21[pi[i]], = the
         //            next La of decoder 1); decisions deinterleaved (:1261-1264).
-        SisoSrc<T> src{dec ? p.sys2 : p.sys1, dec ? p.par2 : p.par1,
-                       dec ? p.ext12 : (it == 0 ? nullptr : p.ext21), p.K, 1};
+        SisoSrc<T> src{dec ? p.sys2 : p.sys1, dec ? p.par2 : p.par1, dec ? p.ext12 : p.ext21, p.K,
+                       (dec == 0 && it == 0) ? 0 : p.K, 1};
         SisoDst<T> dst{dec ? p.ext21 : p.ext12, dec ? 2 : 3, p.K, nullptr, p.le_dump,
                        want_bits ? p.bits : nullptr, p.all_iters ? it : 0, p.all_iters ? p.iters * p.K : p.K,
                        s, p.iters * 2 * p.L};
@@ -707,7 +750,7 @@ __global__ __launch_bounds__(256, 2) void siso_kernel(DecodeParams<T> p, const T
     if (wave == 1) __builtin_amdgcn_s_setprio(2);
     __syncthreads();
     Geom gm{p.K, p.L, p.nT, p.B, (int)blockIdx.x, p.pi, p.pinv};
-    SisoSrc<T> s{p.sys1, p.par1, la, p.L, terminated};
+    SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
     SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0};
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
 }
