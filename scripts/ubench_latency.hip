@@ -84,6 +84,32 @@ __global__ void k(double* out, double a, unsigned long long* cyc, int mode)
                 }
             }
             break;
+        case 11:  // ds_bpermute lookup of a 64-bit value held across lanes (addr from data) + add
+            {
+                const double tv = 1e-9 * threadIdx.x;
+                const int lo = (int)(unsigned)__double_as_longlong(tv), hi = (int)(__double_as_longlong(tv) >> 32);
+                for (int i = 0; i < N; ++i) {
+                    const int q = ((int)(__double_as_longlong(x) >> 40) & 63) << 2;
+                    const int rl = __builtin_amdgcn_ds_bpermute(q, lo), rh = __builtin_amdgcn_ds_bpermute(q, hi);
+                    x = x + __longlong_as_double(((long long)(unsigned)rh << 32) | (unsigned)rl);
+                }
+            }
+            break;
+        case 12:  // three ds_read_b64 (thr, lo, hi) + cmp/select + add (the max* table path)
+            for (int i = 0; i < N; ++i) {
+                const int q = (int)(__double_as_longlong(x) >> 40) & 63;
+                const double t = lds[q], l = lds[64 + q], h = lds[128 + q];
+                x = x + (fabs(x) >= t ? h : l);
+            }
+            break;
+        case 13:  // bucket int ops only: bfe + med3 + lshl (dependent) feeding an add
+            for (int i = 0; i < N; ++i) {
+                const unsigned hi = (unsigned)((unsigned long long)__double_as_longlong(x) >> 32);
+                int q = (int)__builtin_amdgcn_ubfe(hi, 17, 14);
+                q = min(max(q, 8152), 8152 + 56);
+                x = x + (double)(q * 8);
+            }
+            break;
         case 8:   // v_add_f64 pairs interleaved (2 independent chains)
             {
                 double y = x * 0.5;
@@ -108,8 +134,9 @@ int main()
     hipMalloc(&cyc, 64 * sizeof(unsigned long long));
     const char* names[] = {"v_add_f64", "v_fma_f64", "v_max_f64+add0", "dpp64+add_f64", "ds_read_b64(idx)+add",
                            "v_add_f32", "gmax3(dpp+max)+add", "int bfe+med3+lshl", "2x add_f64 interleaved",
-                           "alpha step maxlog (regs)", "alpha step maxlog (lds g)"};
-    for (int mode = 0; mode < 11; ++mode) {
+                           "alpha step maxlog (regs)", "alpha step maxlog (lds g)", "ds_bpermute x2 lookup+add",
+                           "3x ds_read_b64 + sel + add", "bfe+med3+cvt+add"};
+    for (int mode = 0; mode < 14; ++mode) {
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);
         hipDeviceSynchronize();
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);

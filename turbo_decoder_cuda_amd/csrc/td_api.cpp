@@ -129,7 +129,7 @@ Carve carve(int G, int K, size_t elem)
     const int L = K + td::kMemory;
     const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
     const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
-    const size_t arrA = align_up((size_t)G * L * 64 * elem, 256);
+    const size_t arrA = align_up(((size_t)G * L + td::window_steps()) * 64 * elem, 256);   // + one window: DMA tail
     Carve c{};
     c.sys1 = 0;
     c.par1 = c.sys1 + arrL;
@@ -162,11 +162,17 @@ int ensure_ws(td_handle* h, int G)
     return TD_OK;
 }
 
+int groups_for(int B)
+{
+    const int gw = td::groups_per_wg();
+    return ((B + 8 * gw - 1) / (8 * gw)) * gw;   // groups of 8 codewords, whole workgroups
+}
+
 template <typename T>
 int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                     hipStream_t st)
 {
-    const int G = (B + 7) / 8;
+    const int G = groups_for(B);
     int rc = ensure_ws(h, G);
     if (rc) return rc;
     const Carve c = carve(G, h->p.K, sizeof(T));
@@ -216,11 +222,11 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
 template <typename T>
 int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B)
 {
-    const int G = (B + 7) / 8;
+    const int G = groups_for(B);
     const int W = td::window_steps();
     const int nT = (L + W - 1) / W;
     const size_t eL = (size_t)G * L * 8 * sizeof(T);
-    const size_t eA = (size_t)G * L * 64 * sizeof(T);
+    const size_t eA = ((size_t)G * L + td::window_steps()) * 64 * sizeof(T);
     const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
     char* buf = nullptr;
     const size_t eP = (size_t)L * sizeof(int);   // zero permutation tables: the bare SISO writes no extrinsic
@@ -402,7 +408,7 @@ int td_reserve(td_handle* h, int B)
 {
     if (!h || B < 1) return fail(TD_EINVAL, "td_reserve: bad argument");
     TD_HIP(hipSetDevice(h->p.device));
-    return ensure_ws(h, (B + 7) / 8);
+    return ensure_ws(h, groups_for(B));
 }
 
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,

@@ -65,5 +65,6 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
                        hipStream_t st);
 
 int window_steps();
+int groups_per_wg();   // codeword groups (of 8) per workgroup: G must be a multiple of this
 
 }  // namespace td

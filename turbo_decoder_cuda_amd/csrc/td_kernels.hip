@@ -176,16 +176,25 @@ __device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneC
 //                         codeword) item per lane, both input bits in the same lane.
 // Only the two recursions are serial chains; nothing else waits on them but the barriers.  The
 // barriers are raw `s_waitcnt lgkmcnt(0); s_barrier`, so prefetched global loads stay in flight.
-constexpr int kWaves = 4;
+constexpr int kWaves = 4;                            // waves per codeword group
+#ifndef TD_GROUPS_PER_WG
+#define TD_GROUPS_PER_WG 1
+#endif
+#ifndef TD_ROLE_XOR
+#define TD_ROLE_XOR 1
+#endif
+// Codeword groups per workgroup.  With two, the groups run in lock step (shared barriers) and the
+// second group permutes its roles (role = (wave & 3) ^ TD_ROLE_XOR) so that waves w and w+4, which
+// share a SIMD, never hold the same role: the two alpha chains of the forward pass get a SIMD each.
+constexpr int kGroupsPerWg = TD_GROUPS_PER_WG;
 constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (A and F1) per window
 static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
-
 template <typename T>
 struct Smem {
     T lut[3 * kLutPad];        // max* table: thr[64] | vlo[64] | vhi[64]
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
-    T Av[2][kW][kLanes];       // [window parity] alpha[.][i] by 8c + state (fold input)
+    T Av[3][kW][kLanes];       // [window mod 3] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
 };
@@ -256,13 +265,68 @@ __device__ __forceinline__ T la_at(const SisoSrc<T>& src, int i, T raw)
 // ---- tile loader (wave F0): element e = lane and e = lane + 64 (< kTile) of a window
 constexpr int kLoadPerLane = (kTile + kLanes - 1) / kLanes;   // 2
 
+// ---- loader global loads: explicit instructions with hand-counted vmcnt waits.  The compiler
+// sees these loads as completed at issue, so it inserts no waits of its own (its conservative
+// merging across the two-set pipeline drained the whole queue every window); the loader waits
+// with vm_wait<N>() and then "touches" the set so no use can be scheduled above the wait.
+__device__ __forceinline__ void gload(double& d, const double* p)
+{
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void gload(float& d, const float* p)
+{
+    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void gload(int& d, const int* p)
+{
+    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void gload2(double& a, double& b, const double* p)   // one 16-byte load
+{
+    double2 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    a = v.x;
+    b = v.y;
+}
+__device__ __forceinline__ void gload2(float& a, float& b, const float* p)
+{
+    float2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    a = v.x;
+    b = v.y;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <typename V>
+__device__ __forceinline__ void touch(V& v)
+{
+    asm volatile("" : "+v"(v));
+}
+
 template <typename T>
 struct TileRegs {
     T ys[kLoadPerLane], yp[kLoadPerLane], la[kLoadPerLane];
     int wperm[kLoadPerLane], wbit[kLoadPerLane];
 };
+constexpr int kTileLoads = kLoadPerLane * 5;   // vector-memory instructions per tile_issue
 
-// all loads unconditional (clamped element), so every loader iteration issues the same count
+template <typename T>
+__device__ __forceinline__ void touch(TileRegs<T>& r)
+{
+#pragma unroll
+    for (int q = 0; q < kLoadPerLane; ++q) {
+        touch(r.ys[q]);
+        touch(r.yp[q]);
+        touch(r.la[q]);
+        touch(r.wperm[q]);
+        touch(r.wbit[q]);
+    }
+}
+
+// element e of window t (clamped, so the count of loads never varies); values masked at use
 template <typename T>
 __device__ __forceinline__ void tile_issue(TileRegs<T>& r, const SisoSrc<T>& src, const SisoDst<T>& dst,
                                            const Geom& gm, int t, int lane)
@@ -271,10 +335,15 @@ __device__ __forceinline__ void tile_issue(TileRegs<T>& r, const SisoSrc<T>& src
 #pragma unroll
     for (int q = 0; q < kLoadPerLane; ++q) {
         const int e = min(lane + kLanes * q, kTile - 1);
-        load_elem(src, gm, t, e, r.ys[q], r.yp[q], r.la[q], true);
-        const int ik = min(t * kW + (e >> 3), gm.K - 1);
-        r.wperm[q] = pperm[ik];
-        r.wbit[q] = gm.pi[ik];
+        const int k = e >> 3, c = e & 7;
+        const int i = min(max(t * kW + k, 0), gm.L - 1);
+        const size_t off = ((size_t)gm.g * gm.L + i) * kCw + c;
+        gload(r.ys[q], src.sys + off);
+        gload(r.yp[q], src.par + off);
+        gload(r.la[q], src.la + ((size_t)gm.g * src.la_cap + min(i, src.la_cap - 1)) * kCw + c);
+        const int ik = min(i, gm.K - 1);
+        gload(r.wperm[q], pperm + ik);
+        gload(r.wbit[q], gm.pi + ik);
     }
 }
 
@@ -303,24 +372,32 @@ __device__ __forceinline__ void tile_store(const TileRegs<T>& r, Smem<T>& sm, co
 
 // ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
 // Scratch layout: alpha [g][L][64] by 8c + state, tempmax [g][L][8].
-template <typename T>
-struct AlphaRegs {
-    T a[kW];   // alpha[.][t*kW + k] of this lane's (codeword, state) slot
-};
+// alpha of window t: HBM scratch -> LDS slot t % 3 directly (global_load_lds_dwordx4, no
+// registers): the window's kW rows are one contiguous 6 KiB block on both sides.  Completion is
+// tracked by vmcnt; the loader waits for it before the barrier that publishes the slot.
+constexpr int kAlphaDma = kW * kLanes * 8 / (kLanes * 16);   // dwordx4 copies per window (fp64)
+constexpr int kAlphaDmaF32 = kW * kLanes * 4 / (kLanes * 16);
 
 template <typename T>
-__device__ __forceinline__ void alpha_issue(AlphaRegs<T>& r, const T* astore, const Geom& gm, int t, int lane)
+__device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Geom& gm, int t, int lane)
 {
-    const T* src = astore + (size_t)gm.g * gm.L * kLanes + lane;
+    const int slot = ((t % 3) + 3) % 3;
+    const int tc = max(t, 0);
+    const char* src = reinterpret_cast<const char*>(astore + ((size_t)gm.g * gm.L + (size_t)tc * kW) * kLanes);
+    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(
+        &sm.Av[slot][0][0]));
+    constexpr int n = sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32;
+    // Issued through inline asm (M0 saved and restored around it): with the builtin the compiler
+    // guards every later LDS access of this wave with vmcnt(0), as it cannot tell the copy's LDS
+    // target from the tile slots, which would serialise the loader on each copy.
 #pragma unroll
-    for (int k = 0; k < kW; ++k) r.a[k] = src[(size_t)min(max(t * kW + k, 0), gm.L - 1) * kLanes];
-}
-
-template <typename T>
-__device__ __forceinline__ void alpha_store(const AlphaRegs<T>& r, Smem<T>& sm, int t, int lane)
-{
-#pragma unroll
-    for (int k = 0; k < kW; ++k) sm.Av[t & 1][k][lane] = r.a[k];   // rows past the window end are never read
+    for (int q = 0; q < n; ++q) {
+        unsigned save;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(save)
+                     : "s"(lds + q * (kLanes * 16)), "v"(src + q * (kLanes * 16) + lane * 16)
+                     : "memory");
+    }
 }
 
 template <typename T>
@@ -332,9 +409,14 @@ template <typename T>
 __device__ __forceinline__ void tm_issue(TmRegs<T>& r, const T* tmstore, const Geom& gm, int t, int lane)
 {
     const int e = min(max(t * kW * kCw + 2 * lane, 0), gm.L * kCw - 2);   // clamped: always a valid pair
-    const T* src = tmstore + (size_t)gm.g * gm.L * kCw + e;
-    r.v[0] = src[0];
-    r.v[1] = src[1];
+    gload2(r.v[0], r.v[1], tmstore + (size_t)gm.g * gm.L * kCw + e);      // one instruction
+}
+
+template <typename T>
+__device__ __forceinline__ void touch(TmRegs<T>& r)
+{
+    touch(r.v[0]);
+    touch(r.v[1]);
 }
 
 template <typename T>
@@ -502,7 +584,7 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, int t, int e, const
     const T* g = &sm.G[t % 3][k][c][0];
     const T P = g[0], Q = g[1], ys = g[2], la = g[3];
     const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
-    const T* av = &sm.Av[t & 1][k][c * 8];
+    const T* av = &sm.Av[t % 3][k][c * 8];
     const T* bv = &sm.Bv[t & 1][k][c * 8];
     T a[8], b[8], t0[8], t1[8];
 #pragma unroll
@@ -587,13 +669,17 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         __builtin_amdgcn_s_setprio(0);   // in the B pass the beta wave goes first
     } else if (wave == 2) {
-        // loader, two register sets by window parity, two windows ahead; the loops are unrolled by
-        // two so every set is static: F pass iteration t stores tile t+1 and issues tile t+3.
+        // Loader: two register sets by window parity, unrolled by two so each set is static.
+        // Invariant: at the top of an iteration the set it consumes has fully arrived; every
+        // iteration ends with a wait that leaves only its own issues in flight.
+        // F pass iteration t: store tile t+1, issue tile t+3 (into the same set).
         TileRegs<T> ts0, ts1;
         auto fstep = [&](int t, TileRegs<T>& set) {
             TD_STAMP(f0);
+            touch(set);
             if (t + 1 <= tl) tile_store(set, sm, src, t + 1, lane);
             tile_issue(set, src, dst, gm, min(t + 3, tl), lane);
+            vm_wait<kTileLoads>();   // tile t+2 (other set) has arrived
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
@@ -601,43 +687,52 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             TD_ACC(1, f1, f2);
         };
         tile_issue(ts0, src, dst, gm, 0, lane);
+        vm_wait<0>();
+        touch(ts0);
         tile_store(ts0, sm, src, 0, lane);
         tile_issue(ts1, src, dst, gm, min(1, tl), lane);
         tile_issue(ts0, src, dst, gm, min(2, tl), lane);
+        vm_wait<kTileLoads>();
         wg_sync_lds();
         for (int t = 0; t < nT; t += 2) {
             fstep(t, ts1);
             if (t + 1 < nT) fstep(t + 1, ts0);
         }
-        // B pass iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring),
-        // tempmax of wa (beta, next iteration) and alpha of wa+1 (folds, next iteration), each into
-        // the LDS slot nobody reads this iteration, then issues the same streams two windows lower.
-        AlphaRegs<T> ar;   // alpha: one set, one window ahead (24 VGPRs per set)
+        // B pass iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring) and
+        // tempmax of wa (beta, next iteration) into the LDS slots nobody reads this iteration, issues
+        // the same streams two windows lower, and copies alpha of wa (folded at j+2) straight into
+        // LDS slot wa % 3 (last read at j-1).  All issues are unconditional (clamped windows, a
+        // spare slot at the tail), so the per-iteration count kB is fixed.
+        constexpr int kB = kTileLoads + 1 + (sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32);
+        vm_wait<0>();   // the F pass's last (unused) tile loads
         TmRegs<T> ms0, ms1;
         auto bstep = [&](int j, TileRegs<T>& ts, TmRegs<T>& ms) {
             TD_STAMP(b0);
-            const int wa = tl - j, wb = wa + 1;
+            const int wa = tl - j;
+            touch(ts);
+            touch(ms);
             if (wa >= 0 && wa <= tl - 3) tile_store(ts, sm, src, wa, lane);
             if (wa >= 0) tm_store(ms, sm, wa, lane);
-            if (wb >= 0 && wb <= tl) alpha_store(ar, sm, wb, lane);
-            alpha_issue(ar, astore, gm, wb - 1, lane);
             tile_issue(ts, src, dst, gm, max(min(wa - 2, tl - 3), 0), lane);
             tm_issue(ms, tmstore, gm, wa - 2, lane);
+            alpha_dma(sm, astore, gm, wa, lane);
+            vm_wait<kB>();   // last iteration's loads (next iteration's set) and alpha copies landed
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
             TD_ACC(2, b0, b1);
             TD_ACC(3, b1, b2);
         };
-        alpha_issue(ar, astore, gm, tl + 1, lane);             // clamped, never stored
         tile_issue(ts0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never stored
         tm_issue(ms0, tmstore, gm, tl, lane);
         tile_issue(ts1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never stored
         tm_issue(ms1, tmstore, gm, tl - 1, lane);
+        vm_wait<kTileLoads + 1>();   // set 0 arrived
         for (int j = 0; j < nB; j += 2) {
             bstep(j, ts0, ms0);
             if (j + 1 < nB) bstep(j + 1, ts1, ms1);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
     } else {
         wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
@@ -697,23 +792,38 @@ __device__ __forceinline__ void lut_to_lds(const DecodeParams<T>& p, Smem<T>& sm
 }
 
 template <typename T>
-__device__ __forceinline__ Smem<T>& smem()
+__device__ __forceinline__ Smem<T>* smem()
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char td_smem[];
-    return *reinterpret_cast<Smem<T>*>(td_smem);
+    return reinterpret_cast<Smem<T>*>(td_smem);
+}
+
+struct WgPos {
+    int group;   // codeword group within the workgroup
+    int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
+    int lane;
+    int g;       // global codeword group index
+};
+
+__device__ __forceinline__ WgPos wg_pos()
+{
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
+    return WgPos{h, (wave & 3) ^ (h ? TD_ROLE_XOR : 0), (int)(threadIdx.x & 63), (int)blockIdx.x * kGroupsPerWg + h};
 }
 
 // The whole turbo decode of 8 codewords per workgroup (TurboDecoding, log_map.cpp:1146-1280).
 template <typename T, int ALGO>
-__global__ __launch_bounds__(256, 2) void turbo_decode_kernel(DecodeParams<T> p)
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
 {
-    Smem<T>& sm = smem<T>();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    lut_to_lds(p, sm, threadIdx.x);
+    const WgPos w = wg_pos();
+    Smem<T>& sm = smem<T>()[w.group];
+    const int wave = w.role, lane = w.lane;
+    lut_to_lds(p, sm, wave * kLanes + lane);
     if (wave == 1) __builtin_amdgcn_s_setprio(2);   // beta first; alpha raises itself in the F pass
     __syncthreads();
 
-    Geom gm{p.K, p.L, p.nT, p.B, (int)blockIdx.x, p.pi, p.pinv};
+    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     unsigned long long st[kStampSlots] = {};
     // SISO pass s = 2*it + dec
     for (int s = 0; s < 2 * p.iters; ++s) {
@@ -736,20 +846,22 @@ __global__ __launch_bounds__(256, 2) void turbo_decode_kernel(DecodeParams<T> p)
     st[6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
     if (p.stamps && lane == 0)
         for (int q = 0; q < kStampSlots; ++q)
-            p.stamps[((size_t)blockIdx.x * kWaves + wave) * kStampSlots + q] = st[q];
+            p.stamps[((size_t)w.g * kWaves + wave) * kStampSlots + q] = st[q];
 #endif
 }
 
 // Standalone SISO (Log_MAP_decoder) over interleaved [G][L][8] inputs.
 template <typename T, int ALGO>
-__global__ __launch_bounds__(256, 2) void siso_kernel(DecodeParams<T> p, const T* la, int terminated)
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
+                                                                                          int terminated)
 {
-    Smem<T>& sm = smem<T>();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    lut_to_lds(p, sm, threadIdx.x);
+    const WgPos w = wg_pos();
+    Smem<T>& sm = smem<T>()[w.group];
+    const int wave = w.role, lane = w.lane;
+    lut_to_lds(p, sm, wave * kLanes + lane);
     if (wave == 1) __builtin_amdgcn_s_setprio(2);
     __syncthreads();
-    Geom gm{p.K, p.L, p.nT, p.B, (int)blockIdx.x, p.pi, p.pinv};
+    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
     SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0};
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
@@ -851,18 +963,21 @@ inline hipError_t allow_smem(const void* fn, size_t bytes)
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st)
 {
-    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>), sizeof(Smem<T>));
+    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>),
+                              kGroupsPerWg * sizeof(Smem<T>));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
+    hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
+                       kGroupsPerWg * sizeof(Smem<T>), st, p);
     return hipGetLastError();
 }
 
 template <typename T, int ALGO>
 hipError_t launch_siso_algo(const DecodeParams<T>& p, const T* la, int terminated, hipStream_t st)
 {
-    hipError_t e = allow_smem(reinterpret_cast<const void*>(&siso_kernel<T, ALGO>), sizeof(Smem<T>));
+    hipError_t e = allow_smem(reinterpret_cast<const void*>(&siso_kernel<T, ALGO>), kGroupsPerWg * sizeof(Smem<T>));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((siso_kernel<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p, la, terminated);
+    hipLaunchKernelGGL((siso_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
+                       kGroupsPerWg * sizeof(Smem<T>), st, p, la, terminated);
     return hipGetLastError();
 }
 
@@ -907,5 +1022,6 @@ template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*,
                                        hipStream_t);
 
 int window_steps() { return kW; }
+int groups_per_wg() { return kGroupsPerWg; }
 
 }  // namespace td
