@@ -305,6 +305,16 @@ __device__ __forceinline__ void touch(V& v)
 {
     asm volatile("" : "+v"(v));
 }
+// fire-and-forget store pinned in program order against the wave's other memory operations (the
+// scheduler otherwise hoists it onto the recursion's critical path)
+__device__ __forceinline__ void gstore(double* p, double v)
+{
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gstore(float* p, float v)
+{
+    asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
 
 template <typename T>
 struct TileRegs {
@@ -466,15 +476,15 @@ __device__ __forceinline__ T alpha_step(T alpha, T& m_prev, const StepIn<T>& in,
     const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
     T a;
     if constexpr (ALGO == 1) {
-        *pa = alpha;
-        *ptm = m_prev;
+        gstore(pa, alpha);
+        gstore(ptm, m_prev);
         a = vmax(xs, xp);
     } else {
         const T d = xp - xs;
         const int q = bucket_dev<T>(d);
         const T thr = lut[q], lo = lut[kLutPad + q], hi = lut[2 * kLutPad + q];
-        *pa = alpha;
-        *ptm = m_prev;
+        gstore(pa, alpha);   // after the table reads in program order: issued in their shadow
+        gstore(ptm, m_prev);
         a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
     }
     const T m = group_max8(a);
