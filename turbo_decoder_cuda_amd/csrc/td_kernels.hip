@@ -608,8 +608,14 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, int t, int e, const
         t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
         t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
     }
-    const T r0 = fold8<T, ALGO>(t0, sm.lut);
-    const T r1 = fold8<T, ALGO>(t1, sm.lut);
+    // the two folds advanced in lock step (independent chains: twice the latency hidden)
+    T r0 = mstar<T, ALGO>(t0[0], t0[1], sm.lut);
+    T r1 = mstar<T, ALGO>(t1[0], t1[1], sm.lut);
+#pragma unroll
+    for (int j = 2; j < 8; ++j) {
+        r0 = mstar<T, ALGO>(r0, t0[j], sm.lut);
+        r1 = mstar<T, ALGO>(r1, t1[j], sm.lut);
+    }
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
     const int b_ = gm.g * kCw + c;
