@@ -351,6 +351,16 @@ int td_create(td_handle** out, const td_params* p)
     td_handle* h = new td_handle();
     h->p = *p;
     h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
+    {
+        td::LutEntry<double> l64[td::kLutSize];
+        td::LutEntry<float> l32[td::kLutSize];
+        td::build_lut<double>(l64);
+        td::build_lut<float>(l32);
+        if (!td::lut_vhi_is_next_vlo(l64) || !td::lut_vhi_is_next_vlo(l32)) {
+            delete h;
+            return fail(TD_EINVAL, "td_create: max* table does not have the chained form the kernels read");
+        }
+    }
     if (!td::build_trellis(13, 15, h->tr) || !td::build_lane_tables(h->tr, h->lane) || !td::trellis_is_lte(h->tr)) {   // G_ROW_1/2, log_map.h:35-36
         delete h;
         return fail(TD_EINVAL, "td_create: trellis does not fit the rotating-label kernel");

@@ -102,11 +102,13 @@ __device__ __forceinline__ int bucket_dev<float>(float d)
     return min(max(q, BucketBits<float>::base), BucketBits<float>::base + kLutSize - 1) - BucketBits<float>::base;
 }
 
-// The table lives in LDS as three arrays (thr | vlo | vhi, kLutPad entries each): one 8-byte read
-// per field spreads the buckets over 32 bank pairs (a 32-byte AoS entry would leave only 8 bank
-// groups for the 64 lanes' random buckets).
-constexpr int kLutPad = 64;
-static_assert(kLutSize <= kLutPad, "LUT padding");
+// The table lives in LDS as two fields, thr[q] and v[q] (= vlo[q]; vhi[q] = vlo[q+1], see
+// build_lut), each replicated in 16 columns: lane l reads column l % 16, so the 16 lanes an LDS
+// cycle serves always hit 16 distinct bank pairs whatever their buckets (the random buckets of a
+// single shared copy cost ~40% extra LDS cycles in bank conflicts).  `lut` below is the lane's
+// column base (lut_col); vlo[q] and vhi[q] come from one ds_read2_b64.
+constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last bucket
+constexpr int kLutCols = 16;
 
 template <typename T, int ALGO>
 __device__ __forceinline__ T mstar(T x, T y, const T* lut)
@@ -116,7 +118,7 @@ __device__ __forceinline__ T mstar(T x, T y, const T* lut)
     } else {
         const T d = y - x;
         const int q = bucket_dev<T>(d);
-        const T thr = lut[q], lo = lut[kLutPad + q], hi = lut[2 * kLutPad + q];
+        const T thr = lut[q * kLutCols], lo = lut[(kLutRows + q) * kLutCols], hi = lut[(kLutRows + q + 1) * kLutCols];
         return vmax(x, y) + (fabs(d) >= thr ? hi : lo);
     }
 }
@@ -191,7 +193,7 @@ constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (
 static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 template <typename T>
 struct Smem {
-    T lut[3 * kLutPad];        // max* table: thr[64] | vlo[64] | vhi[64]
+    T lut[2 * kLutRows * kLutCols];   // max* table: thr[rows][16] | v[rows][16] (see mstar)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
     T Av[3][kW][kLanes];       // [window mod 3] alpha[.][i] by 8c + state (fold input, DMA from HBM)
@@ -482,7 +484,7 @@ __device__ __forceinline__ T alpha_step(T alpha, T& m_prev, const StepIn<T>& in,
     } else {
         const T d = xp - xs;
         const int q = bucket_dev<T>(d);
-        const T thr = lut[q], lo = lut[kLutPad + q], hi = lut[2 * kLutPad + q];
+        const T thr = lut[q * kLutCols], lo = lut[(kLutRows + q) * kLutCols], hi = lut[(kLutRows + q + 1) * kLutCols];
         gstore(pa, alpha);   // after the table reads in program order: issued in their shadow
         gstore(ptm, m_prev);
         a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
@@ -505,12 +507,12 @@ __device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut
 }
 
 template <typename T, int ALGO>
-__device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, int tb, int k, int c,
+__device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, const T* lut, int tb, int k, int c,
                                           const LaneConst<T>& lc, T* Bvw, const T* tmw)
 {
-    if (ph == 0) return beta_step<T, ALGO, 0>(beta, beta_in<T, 0>(sm, tb, k, c, lc, tmw), sm.lut, k, lc, Bvw);
-    if (ph == 1) return beta_step<T, ALGO, 1>(beta, beta_in<T, 1>(sm, tb, k, c, lc, tmw), sm.lut, k, lc, Bvw);
-    return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), sm.lut, k, lc, Bvw);
+    if (ph == 0) return beta_step<T, ALGO, 0>(beta, beta_in<T, 0>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
+    if (ph == 1) return beta_step<T, ALGO, 1>(beta, beta_in<T, 1>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
+    return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
 }
 
 // alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW.
@@ -518,7 +520,7 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, int
 // caller stores the last one.  At t = 0 the first (meaningless) store lands on index 0, which
 // step 1 then overwrites.
 template <typename T, int ALGO>
-__device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, const Smem<T>& sm, int c,
+__device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, const Smem<T>& sm, const T* lut, int c,
                                           const LaneConst<T>& lc, T* ga, T* gtm)
 {
     const int tb = t % 3;
@@ -531,18 +533,18 @@ __device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, cons
         const StepIn<T> i0 = alpha_in<T, 0>(sm, tb, k, c, lc);
         const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
         const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, i0, sm.lut, lc, pa0 + k * kLanes, ptm);
-        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, i1, sm.lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-        alpha = alpha_step<T, ALGO, 2>(alpha, m_prev, i2, sm.lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, i0, lut, lc, pa0 + k * kLanes, ptm);
+        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+        alpha = alpha_step<T, ALGO, 2>(alpha, m_prev, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
         ptm = gtm + c + (k + 2) * kCw;
     }
     if (k < n) {
-        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), sm.lut, lc, pa0 + k * kLanes,
+        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, pa0 + k * kLanes,
                                        ptm);
         ptm = gtm + c + k * kCw;
     }
     if (k + 1 < n) {
-        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), sm.lut, lc,
+        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc,
                                        pa1 + k * kLanes, ptm);
         ptm = gtm + c + (k + 1) * kCw;
     }
@@ -551,7 +553,7 @@ __device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, cons
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime)
 template <typename T, int ALGO>
-__device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, int c, const LaneConst<T>& lc)
+__device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, const T* lut, int c, const LaneConst<T>& lc)
 {
     const int tb = t % 3, xb = t & 1;
     T* Bvw = &sm.Bv[xb][0][0];
@@ -561,12 +563,12 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, int 
             const StepIn<T> b2 = beta_in<T, 2>(sm, tb, k, c, lc, tmw);
             const StepIn<T> b1 = beta_in<T, 1>(sm, tb, k - 1, c, lc, tmw);
             const StepIn<T> b0 = beta_in<T, 0>(sm, tb, k - 2, c, lc, tmw);
-            beta = beta_step<T, ALGO, 2>(beta, b2, sm.lut, k, lc, Bvw);
-            beta = beta_step<T, ALGO, 1>(beta, b1, sm.lut, k - 1, lc, Bvw);
-            beta = beta_step<T, ALGO, 0>(beta, b0, sm.lut, k - 2, lc, Bvw);
+            beta = beta_step<T, ALGO, 2>(beta, b2, lut, k, lc, Bvw);
+            beta = beta_step<T, ALGO, 1>(beta, b1, lut, k - 1, lc, Bvw);
+            beta = beta_step<T, ALGO, 0>(beta, b0, lut, k - 2, lc, Bvw);
         }
     } else {
-        for (int k = n - 1; k >= 0; --k) beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, tb, k, c, lc, Bvw, tmw);
+        for (int k = n - 1; k >= 0; --k) beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, Bvw, tmw);
     }
     return beta;
 }
@@ -587,7 +589,8 @@ __device__ __forceinline__ T fold8(const T* v, const T* lut)
 // with gamma[p][.][u] = +-P or +-Q (see "gamma"; kTrellisQ) -- the same two roundings as the
 // reference's (gamma + alpha) + beta.  Both folds run in the same lane (independent chains).
 template <typename T, int ALGO>
-__device__ __forceinline__ void fold_item(const Smem<T>& sm, int t, int e, const SisoDst<T>& dst, const Geom& gm)
+__device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t, int e, const SisoDst<T>& dst,
+                                          const Geom& gm)
 {
     const int k = e >> 3, c = e & 7;
     const int i = t * kW + k;
@@ -609,12 +612,12 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, int t, int e, const
         t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
     }
     // the two folds advanced in lock step (independent chains: twice the latency hidden)
-    T r0 = mstar<T, ALGO>(t0[0], t0[1], sm.lut);
-    T r1 = mstar<T, ALGO>(t1[0], t1[1], sm.lut);
+    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
+    T r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
 #pragma unroll
     for (int j = 2; j < 8; ++j) {
-        r0 = mstar<T, ALGO>(r0, t0[j], sm.lut);
-        r1 = mstar<T, ALGO>(r1, t1[j], sm.lut);
+        r0 = mstar<T, ALGO>(r0, t0[j], lut);
+        r1 = mstar<T, ALGO>(r1, t1[j], lut);
     }
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
@@ -671,7 +674,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         wg_sync_lds();
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            alpha = alpha_window<T, ALGO>(alpha, m_prev, t, window_len(gm, t), sm, c, lc,
+            alpha = alpha_window<T, ALGO>(alpha, m_prev, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
                                           ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = m_prev;   // tempmax[L]
@@ -772,7 +775,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = 0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wb = tl - j + 1;
-            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lane >> 3, lc);
+            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -786,7 +789,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             TD_STAMP(b0);
             const int wf = tl - j + 2;
             if (lane < kFoldPerWave && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
-                fold_item<T, ALGO>(sm, wf, fe, dst, gm);
+                fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -799,12 +802,18 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
 template <typename T>
 __device__ __forceinline__ void lut_to_lds(const DecodeParams<T>& p, Smem<T>& sm, int tid)
 {
-    for (int q = tid; q < kLutPad; q += kWaves * kLanes) {
+    for (int e = tid; e < kLutRows * kLutCols; e += kWaves * kLanes) {
+        const int q = e / kLutCols;
         const bool ok = q < kLutSize;
-        sm.lut[q] = ok ? p.lut[q].thr : (T)INFINITY;
-        sm.lut[kLutPad + q] = ok ? p.lut[q].vlo : (T)0;
-        sm.lut[2 * kLutPad + q] = ok ? p.lut[q].vhi : (T)0;
+        sm.lut[e] = ok ? p.lut[q].thr : (T)INFINITY;
+        sm.lut[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
     }
+}
+
+template <typename T>
+__device__ __forceinline__ const T* lut_col(const Smem<T>& sm, int lane)
+{
+    return sm.lut + (lane % kLutCols);
 }
 
 template <typename T>

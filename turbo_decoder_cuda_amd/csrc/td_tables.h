@@ -178,7 +178,18 @@ inline void build_lut(LutEntry<T>* lut)
     }
 }
 
-// Host evaluation of the bucket max* (the device form lives in td_kernels.hip).
+// The device keeps only thr and vlo per bucket and reads vhi[q] as vlo[q+1] (the value just past
+// bucket q's threshold is the value at the start of bucket q+1; buckets without a threshold never
+// read vhi); true for every table build_lut makes -- checked by td_create.
+template <typename T>
+inline bool lut_vhi_is_next_vlo(const LutEntry<T>* lut)
+{
+    for (int q = 0; q + 1 < kLutSize; ++q)   // vhi matters only below a finite threshold
+        if (lut[q].thr < (T)INFINITY && lut[q].vhi != lut[q + 1].vlo) return false;
+    return true;
+}
+
+// Host evaluation of the bucket max* exactly as the device evaluates it (td_kernels.hip mstar).
 template <typename T>
 inline T maxstar_lut_host(T x, T y, const LutEntry<T>* lut)
 {
@@ -186,8 +197,9 @@ inline T maxstar_lut_host(T x, T y, const LutEntry<T>* lut)
     T d = y - x;
     d = d < (T)0 ? -d : d;
     const T m = x > y ? x : y;
-    const LutEntry<T>& e = lut[bucket_of_bits(high_word(d), BB::shift, BB::width, BB::base)];
-    return m + (d >= e.thr ? e.vhi : e.vlo);
+    const int q = bucket_of_bits(high_word(d), BB::shift, BB::width, BB::base);
+    const T hi = q + 1 < kLutSize ? lut[q + 1].vlo : lut[q].vhi;
+    return m + (d >= lut[q].thr ? hi : lut[q].vlo);
 }
 
 }  // namespace td
