@@ -102,6 +102,31 @@ int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le);
  */
 int td_siso_host(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B);
 
+/*
+ * Device frame generator: the frames ITTC/main.cpp makes (main.cpp:170-202)
+ * -- source bits rand() % 2, TurboEnCoding, BPSK, AWGN on I and Q (mgrns, log_map.cpp:1359-1400),
+ * BPSK demodulation (modanddem.cpp:189-224) -- with the process-wide glibc rand() stream of
+ * srand(seed), bit-identical to the reference, generated on the GPU.
+ *   td_synth_seed    srand(seed): (re)starts the handle's frame stream (main.cpp:170)
+ *   td_synth_frames  the next B frames of the stream at Eb/N0 = ebn0_db:
+ *                    d_info [B][K] uint8 source bits, d_llr [B][3K+12] double channel LLRs
+ *                    (TurboDecoding's input).  Synchronous with respect to the host.
+ */
+int td_synth_seed(td_handle* h, unsigned seed);
+/* Position the stream at frame `frame` of srand(seed) (each frame draws K+2 rand() values). */
+int td_synth_seek(td_handle* h, unsigned long long frame);
+/* Host utility behind td_synth_frames (exported for tests): the generator window
+ * x[n-31 .. n-1] of srand(seed) after `draws` rand() calls; the next rand() is
+ * (win[0] + win[28]) >> 1. */
+int td_rand_window(unsigned seed, unsigned long long draws, uint32_t* win);
+int td_synth_frames(td_handle* h, double ebn0_db, int B, uint8_t* d_info, double* d_llr, void* stream);
+
+/* Error counts per frame and iteration for the BER harness (main.cpp:224-237):
+ * d_err[b][it] = #{i < K : d_bits[b][it][i] != d_info[b][i]}, d_bits as td_decode_device's
+ * all_iters output with `iters` rows. */
+int td_count_errors(td_handle* h, const uint8_t* d_bits, int iters, const uint8_t* d_info, int B, int* d_err,
+                    void* stream);
+
 /* Last error message of this thread ("" if none). */
 const char* td_last_error(void);
 /* Number of visible HIP devices (0 on a host without a GPU; never fails). */

@@ -169,3 +169,21 @@ def test_reference_main_links_against_compat():
     exe = os.path.join(REPO, "oracle", "_ref", "main_compat")
     ldd = subprocess.run(["ldd", exe], check=True, capture_output=True, text=True).stdout
     assert "libturbo_logmap_compat.so" in ldd and "libturbo_mi355x.so" in ldd
+
+
+def test_rand_window_jump_matches_glibc_stream():
+    """The generator's jump-ahead (td_rand_window: srand(seed) window advanced by a power of the
+    lagged-Fibonacci companion matrix) continues glibc's rand() stream exactly (the oracle's
+    glibc restatement, itself pinned by the reference's golden frames)."""
+    for seed in (1, 11, 2026):
+        ref = O.glibc_rand_stream(seed, 2600)
+        for d in (0, 1, 30, 31, 100, 2500):
+            w = np.zeros(31, dtype=np.uint32)
+            assert N.lib().td_rand_window(seed, d, w.ctypes.data) == 0
+            x = [int(v) for v in w]
+            outs = []
+            for _ in range(40):
+                v = (x[-31] + x[-3]) & 0xFFFFFFFF
+                x.append(v)
+                outs.append(v >> 1)
+            assert outs == list(ref[d:d + 40])

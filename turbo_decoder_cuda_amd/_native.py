@@ -20,7 +20,7 @@ EXPORTS = (
     "td_create", "td_destroy", "td_reserve", "td_decode_device", "td_decode_host", "td_siso_host",
     "td_last_error", "td_device_count", "td_abi_version", "td_maxstar_host_f64", "td_maxstar_host_f32",
     "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read", "td_debug_set_stamps",
-    "td_debug_stamp_slots",
+    "td_debug_stamp_slots", "td_synth_seed", "td_synth_frames", "td_count_errors", "td_rand_window", "td_synth_seek",
 )
 
 
@@ -69,6 +69,11 @@ def lib() -> C.CDLL:
     L.td_debug_set_stamps.argtypes = [P, P]
     L.td_debug_stamp_slots.restype = I
     L.td_profile_read.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.td_synth_seed.argtypes = [P, C.c_uint]
+    L.td_rand_window.argtypes = [C.c_uint, C.c_ulonglong, P]
+    L.td_synth_seek.argtypes = [P, C.c_ulonglong]
+    L.td_synth_frames.argtypes = [P, C.c_double, I, P, P, P]
+    L.td_count_errors.argtypes = [P, P, I, P, I, P, P]
     _lib = L
     return L
 

@@ -35,7 +35,7 @@ def _run(cmd):
 
 
 def build(force: bool = False, verbose: bool = False) -> None:
-    srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_api.cpp")]
+    srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_synth.hip", "td_api.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
     if force or _newer(LIB, deps):
         extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose else []

@@ -5,6 +5,7 @@
 // CPU fallback: every decode runs on an MI355X or fails with a status code.
 #include <hip/hip_runtime_api.h>
 
+#include <cmath>
 #include <cstdio>
 #include <array>
 #include <cstring>
@@ -57,6 +58,14 @@ struct td_handle {
     bool prof = false;          // td_profile_enable
     std::vector<std::array<hipEvent_t, 3>> ev;   // one triple per profiled decode
     size_t nev = 0;
+    // frame generator (td_synth_seed / td_synth_frames): glibc rand() stream state
+    uint32_t lfg_win[31] = {};                   // x[n-31 .. n-1] before the next draw
+    uint32_t lfg_win0[31] = {};                  // the window right after srand(seed)
+    std::vector<uint32_t> lfg_jump;              // 31x31: window after K+2 draws (one frame)
+    bool lfg_seeded = false;
+    unsigned long long lfg_frames = 0;
+    uint32_t* d_win = nullptr;
+    int win_cap = 0;
 };
 
 namespace td {
@@ -270,6 +279,65 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     return rc;
 }
 
+
+// ---- glibc rand() stream (srandom_r / random_r, TYPE_3: degree 31, separation 3) as the
+// window of the recurrence x[n] = x[n-31] + x[n-3] (mod 2^32), rand() = x[n] >> 1.
+void glibc_window(unsigned seed, uint32_t* win)
+{
+    int32_t tbl[31];
+    if (seed == 0) seed = 1;
+    tbl[0] = (int32_t)seed;
+    long word = (long)seed;
+    for (int i = 1; i < 31; ++i) {   // srandom_r: 16807 * x mod (2^31 - 1), Schrage's method
+        const long hi = word / 127773, lo = word % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        tbl[i] = (int32_t)word;
+    }
+    int f = 3, b = 0;
+    for (int k = 0; k < 310; ++k) {   // srandom_r discards 10 * 31 outputs
+        tbl[f] = (int32_t)((uint32_t)tbl[f] + (uint32_t)tbl[b]);
+        f = (f + 1) % 31;
+        b = (b + 1) % 31;
+    }
+    for (int j = 0; j < 31; ++j) win[j] = (uint32_t)tbl[(f + j) % 31];   // tbl[f] = x[n-31]
+}
+
+// M = A^e where A advances the window by one draw (mod 2^32 arithmetic wraps in uint32_t)
+std::vector<uint32_t> lfg_power(unsigned long long e)
+{
+    auto mul = [](const std::vector<uint32_t>& X, const std::vector<uint32_t>& Y) {
+        std::vector<uint32_t> Z(31 * 31, 0);
+        for (int i = 0; i < 31; ++i)
+            for (int k = 0; k < 31; ++k) {
+                const uint32_t x = X[i * 31 + k];
+                if (!x) continue;
+                for (int j = 0; j < 31; ++j) Z[i * 31 + j] += x * Y[k * 31 + j];
+            }
+        return Z;
+    };
+    std::vector<uint32_t> A(31 * 31, 0), R(31 * 31, 0);
+    for (int j = 0; j < 30; ++j) A[j * 31 + j + 1] = 1;   // W'[j] = W[j+1]
+    A[30 * 31 + 0] = 1;                                    // W'[30] = W[0] + W[28]
+    A[30 * 31 + 28] = 1;
+    for (int i = 0; i < 31; ++i) R[i * 31 + i] = 1;
+    while (e) {
+        if (e & 1) R = mul(R, A);
+        A = mul(A, A);
+        e >>= 1;
+    }
+    return R;
+}
+
+void lfg_apply(const std::vector<uint32_t>& M, const uint32_t* w, uint32_t* out)
+{
+    for (int i = 0; i < 31; ++i) {
+        uint32_t acc = 0;
+        for (int k = 0; k < 31; ++k) acc += M[i * 31 + k] * w[k];
+        out[i] = acc;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -408,6 +476,7 @@ int td_destroy(td_handle* h)
     if (h->d_pinv) (void)hipFree(h->d_pinv);
     if (h->d_lut) (void)hipFree(h->d_lut);
     if (h->d_lane) (void)hipFree(h->d_lane);
+    if (h->d_win) (void)hipFree(h->d_win);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     delete h;
@@ -522,6 +591,77 @@ int td_siso_host(td_handle* h, const void* recs, const void* La, int terminated,
         if (e != hipSuccess) return hip_fail(e, "td_siso_host");
     }
     return rc;
+}
+
+
+int td_rand_window(unsigned seed, unsigned long long draws, uint32_t* win)
+{
+    if (!win) return fail(TD_EINVAL, "td_rand_window: null output");
+    uint32_t w0[31];
+    glibc_window(seed, w0);
+    lfg_apply(lfg_power(draws), w0, win);
+    return TD_OK;
+}
+
+int td_synth_seed(td_handle* h, unsigned seed)
+{
+    if (!h) return fail(TD_EINVAL, "td_synth_seed: null handle");
+    glibc_window(seed, h->lfg_win);
+    std::memcpy(h->lfg_win0, h->lfg_win, sizeof h->lfg_win);
+    if (h->lfg_jump.empty()) h->lfg_jump = lfg_power((unsigned long long)h->p.K + 2);   // K bits + 2 AWGN seeds
+    h->lfg_seeded = true;
+    h->lfg_frames = 0;
+    return TD_OK;
+}
+
+int td_synth_seek(td_handle* h, unsigned long long frame)
+{
+    if (!h || !h->lfg_seeded) return fail(TD_EINVAL, "td_synth_seek: call td_synth_seed first");
+    lfg_apply(lfg_power(frame * ((unsigned long long)h->p.K + 2)), h->lfg_win0, h->lfg_win);
+    h->lfg_frames = frame;
+    return TD_OK;
+}
+
+int td_synth_frames(td_handle* h, double ebn0_db, int B, uint8_t* d_info, double* d_llr, void* stream)
+{
+    if (!h || B < 1 || !d_info || !d_llr) return fail(TD_EINVAL, "td_synth_frames: bad argument");
+    if (!h->lfg_seeded) return fail(TD_EINVAL, "td_synth_frames: call td_synth_seed first");
+    TD_HIP(hipSetDevice(h->p.device));
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (B > h->win_cap) {
+        if (h->d_win) (void)hipFree(h->d_win);
+        h->d_win = nullptr;
+        h->win_cap = 0;
+        if (hipMalloc(&h->d_win, sizeof(uint32_t) * 31 * (size_t)B) != hipSuccess)
+            return fail(TD_ENOMEM, "td_synth_frames: hipMalloc failed");
+        h->win_cap = B;
+    }
+    std::vector<uint32_t> wins((size_t)B * 31);
+    for (int b = 0; b < B; ++b) {
+        std::memcpy(&wins[(size_t)b * 31], h->lfg_win, sizeof h->lfg_win);
+        uint32_t next[31];
+        lfg_apply(h->lfg_jump, h->lfg_win, next);
+        std::memcpy(h->lfg_win, next, sizeof next);
+    }
+    h->lfg_frames += (unsigned long long)B;
+    TD_HIP(hipMemcpyAsync(h->d_win, wins.data(), wins.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    const int K = h->p.K, n = 3 * K + 4 * td::kMemory;
+    const double rate = (double)K / (double)n;                                      // main.cpp:47
+    const double sigma = std::pow(10.0, -ebn0_db / 20) * std::sqrt(0.5 / (rate * 1));   // main.cpp:174
+    td::SynthParams sp{K, n, B, h->d_pi, h->d_win, sigma, 1 / (2 * std::pow(sigma, 2)), d_info, d_llr};
+    TD_HIP(td::launch_synth(sp, st));
+    // the host window buffer must outlive the async copy
+    TD_HIP(hipStreamSynchronize(st));
+    return TD_OK;
+}
+
+int td_count_errors(td_handle* h, const uint8_t* d_bits, int iters, const uint8_t* d_info, int B, int* d_err,
+                    void* stream)
+{
+    if (!h || !d_bits || !d_info || !d_err || B < 1 || iters < 1) return fail(TD_EINVAL, "td_count_errors: bad argument");
+    TD_HIP(hipSetDevice(h->p.device));
+    TD_HIP(td::launch_count_errors(d_bits, d_info, h->p.K, iters, B, d_err, static_cast<hipStream_t>(stream)));
+    return TD_OK;
 }
 
 }  // extern "C"

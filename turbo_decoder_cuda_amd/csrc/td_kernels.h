@@ -64,6 +64,19 @@ template <typename T>
 hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* la_ws, int terminated, T* llr,
                        hipStream_t st);
 
+// device frame generator (td_synth.hip): main.cpp's frame, one thread per frame
+struct SynthParams {
+    int K, n, B;
+    const int* pi;          // [K] QPP
+    const uint32_t* win;    // [B][31] glibc random_r window at each frame's first draw
+    double sigma, Kf;       // main.cpp:174 sigma; demodule's 1/(2 sigma^2), computed on the host
+    uint8_t* info;          // [B][K] source bits out
+    double* flow;           // [B][3K+12] channel LLRs out (fp64, the reference's type)
+};
+hipError_t launch_synth(const SynthParams& p, hipStream_t st);
+hipError_t launch_count_errors(const uint8_t* bits, const uint8_t* info, int K, int iters, int B, int* err,
+                               hipStream_t st);
+
 int window_steps();
 int groups_per_wg();   // codeword groups (of 8) per workgroup: G must be a multiple of this
 

@@ -122,6 +122,42 @@ class TurboCodec:
         N.check(N.lib().td_profile_read(self._h, C.byref(a), C.byref(b), C.byref(n)))
         return a.value, b.value, n.value
 
+    # -- frame generator and error counts (main.cpp's channel, on the device) -------------
+    def synth_seed(self, seed: int) -> None:
+        """srand(seed) for the handle's frame stream (main.cpp:170)."""
+        N.check(N.lib().td_synth_seed(self._h, int(seed) & 0xFFFFFFFF))
+
+    def synth_seek(self, frame: int) -> None:
+        N.check(N.lib().td_synth_seek(self._h, int(frame)))
+
+    def synth(self, B: int, ebn0_db: float, info=None, llr=None, stream=None):
+        """The next B frames of the stream: (info uint8 [B, K], llr float64 [B, 3K+12]) tensors
+        on this codec's device, bit-identical to main.cpp's frames of the same srand seed."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        if info is None:
+            info = torch.empty((B, self.K), dtype=torch.uint8, device=dev)
+        if llr is None:
+            llr = torch.empty((B, stream_length(self.K)), dtype=torch.float64, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        N.check(N.lib().td_synth_frames(self._h, float(ebn0_db), int(B), C.c_void_p(info.data_ptr()),
+                                        C.c_void_p(llr.data_ptr()), C.c_void_p(stream.cuda_stream)))
+        return info, llr
+
+    def count_errors(self, bits, info, stream=None):
+        """bits uint8 [B, iters, K], info uint8 [B, K] -> int32 [B, iters] bit-error counts."""
+        import torch
+
+        B, iters = int(bits.shape[0]), int(bits.shape[1])
+        err = torch.empty((B, iters), dtype=torch.int32, device=bits.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(bits.device)
+        N.check(N.lib().td_count_errors(self._h, C.c_void_p(bits.data_ptr()), iters, C.c_void_p(info.data_ptr()), B,
+                                        C.c_void_p(err.data_ptr()), C.c_void_p(stream.cuda_stream)))
+        return err
+
     # -- Log_MAP_decoder -----------------------------------------------------------------
     def Log_MAP_decoder(self, recs: np.ndarray, La: np.ndarray, terminated: int = TERMINATED) -> np.ndarray:
         """recs [B, 2L] (ys, yp pairs), La [B, L] -> LLR [B, L] (or 1-D for one codeword)."""
