@@ -48,6 +48,10 @@ def lib() -> C.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: build it with `python -m turbo_decoder_cuda_amd.build` "
             "(there is no CPU fallback)")
+    try:   # torch ships its own libamdhip64.so.7 (same soname): load it first so the library and
+        import torch  # noqa: F401  torch bind to one HIP runtime (the other order hides the GPUs from torch)
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P, I = C.c_void_p, C.c_int
     L.td_create.argtypes = [C.POINTER(P), C.POINTER(TdParams)]
