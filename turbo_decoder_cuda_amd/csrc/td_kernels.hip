@@ -469,11 +469,22 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
 // to `pa`) and the previous step's tempmax (`m_prev`, to `ptm`) to HBM scratch.  The stores are
 // issued while the max* table read is in flight, so they cost the chain nothing; nothing ever
 // waits on them inside the pass.
+//
+// The partner's alpha arrives with the step (`ap`): the next step's partner exchange is the first
+// level of this step's 8-lane max (its mask is one of the three the max needs), taken on the
+// unnormalised metric, and both lanes subtract the codeword's common tempmax themselves --
+// fl(a_partner - tempmax) is exactly the partner's alpha, so the exchange leaves the chain.
+template <int PH>
+struct MaxOrder {   // the 8-lane max's DPP masks, the next phase's partner mask first
+    static constexpr int first = PhaseDpp<(PH + 1) % 3>::ctrl;
+    static constexpr int second = PhaseDpp<(PH + 2) % 3>::ctrl;
+    static constexpr int third = PhaseDpp<PH>::ctrl;
+};
+
 template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T alpha_step(T alpha, T& m_prev, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc,
-                                        T* pa, T* ptm)
+__device__ __forceinline__ T alpha_step(T alpha, T& ap, T& m_prev, const StepIn<T>& in, const T* lut,
+                                        const LaneConst<T>& lc, T* pa, T* ptm)
 {
-    const T ap = dpp<PhaseDpp<PH>::ctrl>(alpha);
     const T xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
     const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
     T a;
@@ -489,8 +500,12 @@ __device__ __forceinline__ T alpha_step(T alpha, T& m_prev, const StepIn<T>& in,
         gstore(ptm, m_prev);
         a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
     }
-    const T m = group_max8(a);
+    const T an = dpp<MaxOrder<PH>::first>(a);   // the next step's partner, unnormalised
+    T m = vmax(a, an);
+    m = vmax(m, dpp<MaxOrder<PH>::second>(m));
+    m = vmax(m, dpp<MaxOrder<PH>::third>(m));
     m_prev = m;
+    ap = an - m;
     return a - m;
 }
 
@@ -520,8 +535,8 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
 // caller stores the last one.  At t = 0 the first (meaningless) store lands on index 0, which
 // step 1 then overwrites.
 template <typename T, int ALGO>
-__device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, const Smem<T>& sm, const T* lut, int c,
-                                          const LaneConst<T>& lc, T* ga, T* gtm)
+__device__ __forceinline__ T alpha_window(T alpha, T& ap, T& m_prev, int t, int n, const Smem<T>& sm, const T* lut,
+                                          int c, const LaneConst<T>& lc, T* ga, T* gtm)
 {
     const int tb = t % 3;
     T* pa0 = ga + lc.st_off[0];
@@ -533,18 +548,18 @@ __device__ __forceinline__ T alpha_window(T alpha, T& m_prev, int t, int n, cons
         const StepIn<T> i0 = alpha_in<T, 0>(sm, tb, k, c, lc);
         const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
         const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, i0, lut, lc, pa0 + k * kLanes, ptm);
-        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-        alpha = alpha_step<T, ALGO, 2>(alpha, m_prev, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+        alpha = alpha_step<T, ALGO, 0>(alpha, ap, m_prev, i0, lut, lc, pa0 + k * kLanes, ptm);
+        alpha = alpha_step<T, ALGO, 1>(alpha, ap, m_prev, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+        alpha = alpha_step<T, ALGO, 2>(alpha, ap, m_prev, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
         ptm = gtm + c + (k + 2) * kCw;
     }
     if (k < n) {
-        alpha = alpha_step<T, ALGO, 0>(alpha, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, pa0 + k * kLanes,
+        alpha = alpha_step<T, ALGO, 0>(alpha, ap, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, pa0 + k * kLanes,
                                        ptm);
         ptm = gtm + c + k * kCw;
     }
     if (k + 1 < n) {
-        alpha = alpha_step<T, ALGO, 1>(alpha, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc,
+        alpha = alpha_step<T, ALGO, 1>(alpha, ap, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc,
                                        pa1 + k * kLanes, ptm);
         ptm = gtm + c + (k + 1) * kCw;
     }
@@ -670,11 +685,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         lane_setup(lt, lane, lc);
         T alpha = lc.a_init0 ? (T)0 : (T)-kInfty;   // :943,948
         T m_prev = (T)0;
+        T ap = dpp<PhaseDpp<0>::ctrl>(alpha);   // the first step's partner
         __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            alpha = alpha_window<T, ALGO>(alpha, m_prev, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
+            alpha = alpha_window<T, ALGO>(alpha, ap, m_prev, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
                                           ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = m_prev;   // tempmax[L]
