@@ -191,12 +191,14 @@ constexpr int kWaves = 4;                            // waves per codeword group
 constexpr int kGroupsPerWg = TD_GROUPS_PER_WG;
 constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (A and F1) per window
 static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
+constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
+
 template <typename T>
 struct Smem {
     T lut[2 * kLutRows * kLutCols];   // max* table: thr[rows][16] | v[rows][16] (see mstar)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
-    T Av[3][kW][kLanes];       // [window mod 3] alpha[.][i] by 8c + state (fold input, DMA from HBM)
+    T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
 };
@@ -393,7 +395,7 @@ constexpr int kAlphaDmaF32 = kW * kLanes * 4 / (kLanes * 16);
 template <typename T>
 __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Geom& gm, int t, int lane)
 {
-    const int slot = ((t % 3) + 3) % 3;
+    const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
     const char* src = reinterpret_cast<const char*>(astore + ((size_t)gm.g * gm.L + (size_t)tc * kW) * kLanes);
     const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(
@@ -612,7 +614,7 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     const T* g = &sm.G[t % 3][k][c][0];
     const T P = g[0], Q = g[1], ys = g[2], la = g[3];
     const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
-    const T* av = &sm.Av[t % 3][k][c * 8];
+    const T* av = &sm.Av[t % kAvSlots][k][c * 8];
     const T* bv = &sm.Bv[t & 1][k][c * 8];
     T a[8], b[8], t0[8], t1[8];
 #pragma unroll
@@ -735,12 +737,15 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         // B pass iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring) and
         // tempmax of wa (beta, next iteration) into the LDS slots nobody reads this iteration, issues
-        // the same streams two windows lower, and copies alpha of wa (folded at j+2) straight into
-        // LDS slot wa % 3 (last read at j-1).  All issues are unconditional (clamped windows, a
-        // spare slot at the tail), so the per-iteration count kB is fixed.
+        // the same streams three windows lower into the set it just consumed, and copies alpha of
+        // wa-1 (folded at j+3) straight into LDS slot (wa-1) % 4 (last read at j-1).  All issues are
+        // unconditional (clamped windows, a spare slot at the tail), so the per-iteration count kB
+        // is fixed and every iteration ends leaving only its own and the previous iteration's issues
+        // in flight: three windows of latency for the loads, three for the copies.
         constexpr int kB = kTileLoads + 1 + (sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32);
         vm_wait<0>();   // the F pass's last (unused) tile loads
-        TmRegs<T> ms0, ms1;
+        TileRegs<T> ts2;
+        TmRegs<T> ms0, ms1, ms2;
         auto bstep = [&](int j, TileRegs<T>& ts, TmRegs<T>& ms) {
             TD_STAMP(b0);
             const int wa = tl - j;
@@ -748,10 +753,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             touch(ms);
             if (wa >= 0 && wa <= tl - 3) tile_store(ts, sm, src, wa, lane);
             if (wa >= 0) tm_store(ms, sm, wa, lane);
-            tile_issue(ts, src, dst, gm, max(min(wa - 2, tl - 3), 0), lane);
-            tm_issue(ms, tmstore, gm, wa - 2, lane);
-            alpha_dma(sm, astore, gm, wa, lane);
-            vm_wait<kB>();   // last iteration's loads (next iteration's set) and alpha copies landed
+            tile_issue(ts, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+            tm_issue(ms, tmstore, gm, wa - 3, lane);
+            alpha_dma(sm, astore, gm, wa - 1, lane);
+            vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -762,10 +767,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         tm_issue(ms0, tmstore, gm, tl, lane);
         tile_issue(ts1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never stored
         tm_issue(ms1, tmstore, gm, tl - 1, lane);
-        vm_wait<kTileLoads + 1>();   // set 0 arrived
-        for (int j = 0; j < nB; j += 2) {
+        tile_issue(ts2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never stored
+        tm_issue(ms2, tmstore, gm, tl - 2, lane);
+        alpha_dma(sm, astore, gm, tl, lane);                   // folded at j = 2
+        vm_wait<2 * (kTileLoads + 1) + (sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32)>();   // set 0 arrived
+        for (int j = 0; j < nB; j += 3) {
             bstep(j, ts0, ms0);
             if (j + 1 < nB) bstep(j + 1, ts1, ms1);
+            if (j + 2 < nB) bstep(j + 2, ts2, ms2);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
