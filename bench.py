@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
     ap.add_argument("--cpu-sample", type=int, default=4096, help="codewords for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--window", type=int, default=0, help="0 = exact schedule; 64 = sliding window (config 5)")
+    ap.add_argument("--overlap", type=int, default=30, help="sliding-window warm-up steps")
     ap.add_argument("--no-variants", action="store_true")
     return ap.parse_args()
 
@@ -94,6 +96,8 @@ def main():
     u_d = torch.from_numpy(u).to(dev)
 
     codec = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=local)
+    if a.window:
+        codec.set_window(a.window, a.overlap)
     codec.reserve(a.batch)
     bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -159,7 +163,8 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     bytes_cw = esz * (3 * a.K + 12) + a.K   # algorithmic: LLR in + uint8 bits out
     alg_bytes = bytes_cw * a.batch
     achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9 if turbo_ms > 0 else 0.0
-    cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}"
+    cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}" + (f"_w{a.window}g{a.overlap}" if a.window else "")
+    cfg_no = "5" if a.window else ("2" if a.algo == "logmap" else "3")
     return {
         "metric": METRIC,
         "value": round(value, 3),
@@ -174,17 +179,18 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
         "dtype": a.precision,
         "data": "synthetic: PCG64 info bits, RSC 13/15 + QPP turbo encoder, BPSK, AWGN (numpy), LLR=2y/sigma^2",
         "config": {
-            "workload": f"BASELINE config {'2' if a.algo == 'logmap' else '3'}: batch {a.batch} x K={a.K} per GPU, "
+            "workload": f"BASELINE config {cfg_no}: batch {a.batch} x K={a.K} per GPU, "
                         f"{a.iters} iterations, {'log-MAP table max*' if a.algo == 'logmap' else 'Max-Log-MAP'}, "
                         f"{a.precision} {'parity (reference op order)' if a.precision == 'f64' else 'throughput'}, "
-                        f"Eb/N0={a.ebn0} dB",
+                        f"Eb/N0={a.ebn0} dB" + (f", sliding window {a.window} with overlap {a.overlap}" if a.window else ""),
             "K": a.K, "f1": f1, "f2": f2, "batch_per_gpu": a.batch, "global_batch": a.batch * world,
             "iterations": a.iters, "algo": a.algo, "precision": a.precision, "ebn0_db": a.ebn0,
+            "window": a.window, "overlap": a.overlap if a.window else None,
             "parallelism": f"batch-shard x{world} (no collective on the data path)",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "turbo_decode_kernel",
+            "kernel": "sw_siso_kernel" if a.window else "turbo_decode_kernel",
             "achieved": round(achieved, 3),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -255,11 +261,15 @@ def variants(a, llr64, u_d, f1, f2, dev, stream):
     from turbo_decoder_cuda_amd import TurboCodec
 
     res = {}
-    for prec, algo in (("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog")):
-        if prec == a.precision and algo == a.algo:
+    cases = [(p, g, 0) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog"))]
+    cases += [(p, g, 64) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
+    for prec, algo, win in cases:
+        if prec == a.precision and algo == a.algo and win == a.window:
             continue
         x = llr64 if prec == "f64" else llr64.float()
         c = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=algo, precision=prec, device=dev.index)
+        if win:
+            c.set_window(win, a.overlap)
         c.reserve(a.batch)
         b = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
         c.decode(x, b, stream=stream)
@@ -274,7 +284,7 @@ def variants(a, llr64, u_d, f1, f2, dev, stream):
         _, kms, _ = c.kernel_ms()
         c.close()
         errs = int((b != u_d).sum().item())
-        res[f"{prec}_{algo}"] = {"value": round(a.batch * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s",
+        res[f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else "")] = {"value": round(a.batch * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s",
                                  "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4),
                                  "bit_errors": errs}
     return res

@@ -77,6 +77,18 @@ int td_reserve(td_handle* h, int B);
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                      void* stream);
 
+/*
+ * Decoding schedule of the handle (BASELINE config 5).  window = 0 (the
+ * default) is the exact full-trellis schedule of log_map.cpp.  window = 64 cuts each codeword's
+ * trellis into sub-blocks of 64 steps decoded in parallel (sliding-window BCJR): a sub-block's
+ * alpha starts `overlap` steps early and its beta `overlap` steps late from equal metrics
+ * (overlap initialisation; 0 <= overlap <= 3*64, a multiple of 3), the extrinsic is multiplied by
+ * ext_scale (1 = none; the reference GPU variants use 0.77, turboDecoderBianJieZhi.cu:423-434).
+ * Windowed decoding changes the arithmetic: its parity gate is the BER curve, not bit-exactness.
+ * Reference: the sub-block CUDA decoders ITTC/CUDA/turboDecoder.cu:20-21,205-331.
+ */
+int td_set_window(td_handle* h, int window, int overlap, float ext_scale);
+
 /* Kernel timing (measurement support): while enabled, hipEvents on the decode stream bracket
  * the demultiplex kernel and the turbo kernel of every td_decode_device call.
  * td_profile_read synchronises on them, returns the average durations (ms) over the

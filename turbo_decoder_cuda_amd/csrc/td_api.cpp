@@ -66,6 +66,9 @@ struct td_handle {
     unsigned long long lfg_frames = 0;
     uint32_t* d_win = nullptr;
     int win_cap = 0;
+    // decoding schedule (td_set_window): 0 = exact full trellis
+    int window = 0;
+    td::WindowParams wp{0, 1.0f};
 };
 
 namespace td {
@@ -222,8 +225,8 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     hipError_t e = td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
-    e = td::launch_turbo<T>(dp, st);
-    if (e != hipSuccess) return hip_fail(e, "launch_turbo");
+    e = h->window ? td::launch_window<T>(dp, h->wp, st) : td::launch_turbo<T>(dp, st);
+    if (e != hipSuccess) return hip_fail(e, h->window ? "launch_window" : "launch_turbo");
     if (ev) TD_HIP(hipEventRecord(ev[2], st));
     return TD_OK;
 }
@@ -498,6 +501,19 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (h->p.precision == TD_F64) return decode_device_t<double>(h, d_llr, B, d_bits, all_iters, d_le, st);
     return decode_device_t<float>(h, d_llr, B, d_bits, all_iters, d_le, st);
+}
+
+int td_set_window(td_handle* h, int window, int overlap, float ext_scale)
+{
+    if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
+    if (window != 0 && window != td::sliding_window_steps())
+        return fail(TD_EINVAL, "td_set_window: window must be 0 (exact) or " + std::to_string(td::sliding_window_steps()));
+    if (overlap < 0 || overlap > 3 * td::sliding_window_steps() || overlap % 3)
+        return fail(TD_EINVAL, "td_set_window: overlap must be a multiple of 3 in [0, 3*window]");
+    if (!(ext_scale > 0.0f) || !(ext_scale <= 4.0f)) return fail(TD_EINVAL, "td_set_window: ext_scale must be in (0, 4]");
+    h->window = window;
+    h->wp = td::WindowParams{overlap, ext_scale};
+    return TD_OK;
 }
 
 int td_profile_enable(td_handle* h, int on)

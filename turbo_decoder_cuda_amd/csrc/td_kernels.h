@@ -60,6 +60,14 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 template <typename T>
 hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st);
 
+// sliding-window mode (BASELINE config 5): sub-blocks of 64 steps with `overlap` warm-up steps
+struct WindowParams {
+    int overlap;       // warm-up steps (multiple of 3)
+    float ext_scale;   // extrinsic scaling (1 = none)
+};
+template <typename T>
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st);
+
 template <typename T>
 hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* la_ws, int terminated, T* llr,
                        hipStream_t st);
@@ -78,6 +86,7 @@ hipError_t launch_count_errors(const uint8_t* bits, const uint8_t* info, int K, 
                                hipStream_t st);
 
 int window_steps();
+int sliding_window_steps();   // sub-block length of launch_window (64)
 int groups_per_wg();   // codeword groups (of 8) per workgroup: G must be a multiple of this
 
 }  // namespace td

@@ -917,6 +917,207 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
 }
 
+// ================================================================== sliding-window mode
+// BASELINE config 5 / SURVEY.md 8f row 3: the trellis of each codeword is cut into sub-blocks of
+// W steps decoded in parallel.  A sub-block's alpha starts g steps early from equal metrics
+// (overlap initialisation) and its beta g steps late; only the codeword's first alpha and last
+// beta start from the true initial / terminated states.  Each 8-lane group of a wave holds one
+// (codeword, sub-block) pair, so a wave runs 8 independent chains and thousands of waves are in
+// flight: this mode is throughput-bound, not latency-bound.  It is NOT the reference's
+// arithmetic: the windows' boundary metrics are approximations, the LLR fold is a butterfly (tree
+// order) max*, and the extrinsic may be scaled (ext_scale).  The SISO schedule is the
+// reference's serial one (one launch per SISO).
+//
+// Labels rotate with the step index relative to the chain's origin i0 = s*W - g (the trellis is
+// time-invariant), so the 8 groups of a wave stay in phase whatever their absolute steps; slot 0
+// holds state 0 at every phase.
+struct WinArgs {
+    int W, g;          // sub-block length, overlap
+    int nS;            // sub-blocks per codeword
+    float ext_scale;
+    int dec, it;       // SISO 0/1, iteration
+};
+
+template <typename T>
+struct SwIn {
+    T P, Q, ys, la;
+};
+
+// channel + a-priori of (codeword b, step i) for decoder `dec` (steps outside [0, L) clamped)
+template <typename T>
+__device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, int dec, int la_len, int b, int i)
+{
+    const int ic = min(max(i, 0), p.L - 1);
+    const size_t off = ((size_t)(b >> 3) * p.L + ic) * kCw + (b & 7);
+    const T ys = (dec ? p.sys2 : p.sys1)[off];
+    const T yp = (dec ? p.par2 : p.par1)[off];
+    const T* la_arr = dec ? p.ext12 : p.ext21;
+    const T lr = la_arr[((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
+    const T la = ic < la_len ? lr : (T)0;
+    const T hla = la / (T)2;
+    return SwIn<T>{(ys + yp) + hla, (ys - yp) + hla, ys, la};
+}
+
+// one alpha step of phase PH on a group's metric (normalised by the group max); `freeze` keeps it
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T sw_alpha_step(T alpha, const SwIn<T>& in, const T* lut, const LaneConst<T>& lc, bool freeze)
+{
+    const T gs = lc.a_sel[PH] ? in.Q : in.P, gp = lc.a_psel[PH] ? in.Q : in.P;
+    const T ap = dpp<PhaseDpp<PH>::ctrl>(alpha);
+    const T a = mstar<T, ALGO>(fma(lc.a_sg[PH], gs, alpha), fma(lc.a_pg[PH], gp, ap), lut);
+    const T m = group_max8(a);
+    return freeze ? alpha : a - m;
+}
+
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T sw_beta_step(T beta, const SwIn<T>& in, const T* lut, const LaneConst<T>& lc, bool freeze)
+{
+    const T gs = lc.b_sel[PH] ? in.Q : in.P, gp = lc.b_psel[PH] ? in.Q : in.P;
+    const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
+    const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], gs, beta), fma(lc.b_pg[PH], gp, bp), lut);
+    const T m = group_max8(b);
+    return freeze ? beta : b - m;
+}
+
+// max* over the 8 lanes of a group, butterfly (every lane gets the tree result)
+template <typename T, int ALGO>
+__device__ __forceinline__ T sw_group_mstar(T v, const T* lut)
+{
+    v = mstar<T, ALGO>(v, dpp<kDppXor1>(v), lut);
+    v = mstar<T, ALGO>(v, dpp<kDppXor2>(v), lut);
+    v = mstar<T, ALGO>(v, dpp<kDppMir8>(v), lut);
+    return v;
+}
+
+template <typename T>
+struct SwCtx {
+    const DecodeParams<T>& p;
+    const WinArgs& a;
+    const LaneConst<T>& lc;
+    const T* lut;
+    int b, s, la_len, i0;
+    bool live;
+    int slot;
+    bool want_bits;
+};
+
+// beta step at relative index kr (absolute i = i0 + kr, phase PH = kr % 3), with the LLR fold of
+// step i when i lies in the sub-block: the lane's two LLR terms belong to the next state its
+// beta[.][i+1] is held for (the alpha step's self / partner transitions)
+template <typename T, int ALGO, int PH, int W>
+__device__ __forceinline__ T sw_beta_fold(const SwCtx<T>& cx, T beta, int kr)
+{
+    const DecodeParams<T>& p = cx.p;
+    const LaneConst<T>& lc = cx.lc;
+    const int i = cx.i0 + kr;
+    const SwIn<T> x = sw_load(p, cx.a.dec, cx.la_len, cx.b, i);
+    if (kr < cx.a.g + W && i < p.L) {
+        const T al = p.astore[((size_t)(cx.b >> 3) * p.L + i) * kLanes + (cx.b & 7) * 8 + lc.st_off[PH] - (threadIdx.x & 56)];
+        const T gs = lc.a_sel[PH] ? x.Q : x.P, gp = lc.a_psel[PH] ? x.Q : x.P;
+        const T alp = dpp<PhaseDpp<PH>::ctrl>(al);
+        const T xs = fma(lc.a_sg[PH], gs, al) + beta, xp = fma(lc.a_pg[PH], gp, alp) + beta;
+        const bool us = lc.a_sg[PH] > (T)0;
+        const T m1 = sw_group_mstar<T, ALGO>(us ? xs : xp, cx.lut), m0 = sw_group_mstar<T, ALGO>(us ? xp : xs, cx.lut);
+        const T llr = m1 - m0;
+        if (cx.live && cx.slot == 0) {
+            const T le = (llr - x.la - (T)2 * x.ys) * (T)cx.a.ext_scale;
+            const int c = cx.b & 7, g8 = cx.b >> 3;
+            if (i < p.K) {
+                const int w = cx.a.dec ? p.pi[i] : p.pinv[i];
+                T* ext = cx.a.dec ? p.ext21 : p.ext12;
+                ext[((size_t)g8 * p.K + w) * kCw + c] = le;
+                if (cx.want_bits)
+                    p.bits[(size_t)cx.b * (p.all_iters ? p.iters * p.K : p.K) +
+                           (size_t)(p.all_iters ? cx.a.it : 0) * p.K + p.pi[i]] = llr < (T)0 ? 0 : 1;
+            }
+            if (p.le_dump) p.le_dump[(size_t)cx.b * p.iters * 2 * p.L + (size_t)(2 * cx.a.it + cx.a.dec) * p.L + i] = le;
+        }
+    }
+    return sw_beta_step<T, ALGO, PH>(beta, x, cx.lut, lc, i + 1 > p.L);   // beyond the end: hold the init
+}
+
+template <typename T, int ALGO, int W>
+__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs a)
+{
+    __shared__ T lut_s[2 * kLutRows * kLutCols];
+    for (int e = threadIdx.x; e < kLutRows * kLutCols; e += blockDim.x) {
+        const int q = e / kLutCols;
+        const bool ok = q < kLutSize;
+        lut_s[e] = ok ? p.lut[q].thr : (T)INFINITY;
+        lut_s[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, slot = lane & 7;
+    const T* lut = lut_s + (lane % kLutCols);
+    LaneConst<T> lc;
+    lane_setup(p.lane, lane, lc);
+    const int task = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (lane >> 3);
+    const bool live = task < p.B * a.nS;
+    const int b = live ? task / a.nS : 0, s = live ? task % a.nS : 0;
+    const int la_len = (a.dec == 0 && a.it == 0) ? 0 : p.K;
+    const int i0 = s * W - a.g;   // absolute step of relative index 0
+
+    // ---- alpha: g warm-up steps then the W steps of the sub-block, stored by state in the
+    // alpha scratch ([G][L][64], L2-resident between the two passes)
+    const T init = slot == 0 ? (T)0 : (T)-kInfty;
+    T alpha = i0 <= 0 ? init : (T)0;   // i0 <= 0: the chain reaches (or starts at) step 0
+    T* arow = p.astore + ((size_t)(b >> 3) * p.L) * kLanes + (b & 7) * 8;
+    for (int k = 0; k + 3 <= a.g + W; k += 3) {   // g + W = 0 mod 3 is not required: tail below
+        const int i = i0 + k;
+        const SwIn<T> x0 = sw_load(p, a.dec, la_len, b, i), x1 = sw_load(p, a.dec, la_len, b, i + 1),
+                      x2 = sw_load(p, a.dec, la_len, b, i + 2);
+        if (live && i >= s * W && i < p.L) arow[(size_t)i * kLanes + lc.st_off[0] - (lane & ~7)] = alpha;
+        alpha = sw_alpha_step<T, ALGO, 0>(alpha, x0, lut, lc, i < 0);
+        if (live && i + 1 >= s * W && i + 1 < p.L) arow[(size_t)(i + 1) * kLanes + lc.st_off[1] - (lane & ~7)] = alpha;
+        alpha = sw_alpha_step<T, ALGO, 1>(alpha, x1, lut, lc, i + 1 < 0);
+        if (live && i + 2 >= s * W && i + 2 < p.L) arow[(size_t)(i + 2) * kLanes + lc.st_off[2] - (lane & ~7)] = alpha;
+        alpha = sw_alpha_step<T, ALGO, 2>(alpha, x2, lut, lc, i + 2 < 0);
+    }
+    {   // W = 64 = 1 mod 3: the last stored step (phase 0)
+        const int i = i0 + ((a.g + W) / 3) * 3;
+        if (live && i >= s * W && i < p.L && i < s * W + W) arow[(size_t)i * kLanes + lc.st_off[0] - (lane & ~7)] = alpha;
+    }
+
+    // ---- beta: g warm-up steps down to the sub-block's end, then the W steps with the LLR fold;
+    // relative index kr = i - i0 from W + 2g - 1 (= 0 mod 3) down to g, phases 0, 2, 1, ...
+    const int e_end = s * W + W + a.g;   // absolute index of the first beta (beta[.][e_end])
+    T beta = e_end >= p.L ? init : (T)0;
+    SwCtx<T> cx{p, a, lc, lut, b, s, la_len, i0, live, slot, a.dec == 1 && (p.all_iters || a.it == p.iters - 1)};
+    int kr = W + 2 * a.g - 1;
+    for (; kr - 2 >= a.g; kr -= 3) {
+        beta = sw_beta_fold<T, ALGO, 0, W>(cx, beta, kr);
+        beta = sw_beta_fold<T, ALGO, 2, W>(cx, beta, kr - 1);
+        beta = sw_beta_fold<T, ALGO, 1, W>(cx, beta, kr - 2);
+    }
+    if (kr >= a.g) beta = sw_beta_fold<T, ALGO, 0, W>(cx, beta, kr);   // W + g = 1 mod 3: one step left
+}
+
+constexpr int kSwW = 64;   // compiled sub-block length (BASELINE config 5)
+
+template <typename T, int ALGO>
+hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st)
+{
+    const int nS = (p.L + kSwW - 1) / kSwW;
+    const long long tasks = (long long)p.B * nS;
+    const int blocks = (int)((tasks + 31) / 32);   // 4 waves x 8 groups per block
+    for (int it = 0; it < p.iters; ++it)
+        for (int dec = 0; dec < 2; ++dec) {
+            WinArgs a{kSwW, w.overlap, nS, w.ext_scale, dec, it};
+            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO, kSwW>), dim3(blocks), dim3(256), 0, st, p, a);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+int sliding_window_steps() { return kSwW; }
+
+template <typename T>
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st)
+{
+    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, st) : launch_window_algo<T, 0>(p, w, st);
+}
+
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
 // batch-interleaved arrays.  One thread per (group, step, codeword).
 template <typename T>
@@ -1065,6 +1266,8 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t);
+template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, hipStream_t);
+template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, hipStream_t);
 template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);

@@ -66,6 +66,11 @@ class TurboCodec:
     def reserve(self, B: int) -> None:
         N.check(N.lib().td_reserve(self._h, int(B)))
 
+    def set_window(self, window: int = 64, overlap: int = 32 // 3 * 3, ext_scale: float = 1.0) -> None:
+        """Sliding-window schedule (td_set_window; BASELINE config 5). window=0: exact schedule."""
+        N.check(N.lib().td_set_window(self._h, int(window), int(overlap), float(ext_scale)))
+        self.window = int(window)
+
     # -- TurboDecoding, host arrays ------------------------------------------------------
     def TurboDecoding(self, flow: np.ndarray, return_le: bool = False):
         """flow [B, 3K+12] (or one row) -> out int32 [B, iterations, K] (the reference's
