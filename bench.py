@@ -35,7 +35,7 @@ FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (half the FP32 vector rate, 1
 F1, F2 = 263, 480             # QPP for K=6144 (ITTC/main.cpp:36-37)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--window", type=int, default=0, help="0 = exact schedule; 64 = sliding window (config 5)")
     ap.add_argument("--overlap", type=int, default=30, help="sliding-window warm-up steps")
     ap.add_argument("--no-variants", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def qpp_for(K):

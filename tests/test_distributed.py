@@ -1,7 +1,6 @@
 """Multi-rank bench logic on CPU (gloo, world_size 2): each rank decodes its own shard of
 codewords, so the only exchange is the max of the timed-region wall time and the sum of the
 error counters (bench.reduce_over_ranks); value = all ranks' info bits / max time."""
-import argparse
 import os
 import socket
 
@@ -28,8 +27,7 @@ def _worker(rank, world, port, q):
     elapsed = [2.0, 2.5][rank]
     errs, blk = [10, 3][rank], [1, 2][rank]
     e, n, b = bench.reduce_over_ranks(elapsed, errs, blk, world)
-    a = argparse.Namespace(steps=4, warmup=1, batch=64, K=1024, iters=8, ebn0=1.0, precision="f64",
-                           algo="logmap")
+    a = bench.parse(["--steps", "4", "--warmup", "1", "--batch", "64", "--K", "1024"])
     rec = bench.summarize(a, world, e, n, b, 0.1, 100.0, 4, 31, 64)
     q.put((rank, e, n, b, rec))
     dist.barrier()
