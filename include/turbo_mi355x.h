@@ -78,16 +78,26 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
                      void* stream);
 
 /*
- * Decoding schedule of the handle (BASELINE config 5).  window = 0 (the
- * default) is the exact full-trellis schedule of log_map.cpp.  window = 64 cuts each codeword's
- * trellis into sub-blocks of 64 steps decoded in parallel (sliding-window BCJR): a sub-block's
- * alpha starts `overlap` steps early and its beta `overlap` steps late from equal metrics
- * (overlap initialisation; 0 <= overlap <= 3*64, a multiple of 3), the extrinsic is multiplied by
- * ext_scale (1 = none; the reference GPU variants use 0.77, turboDecoderBianJieZhi.cu:423-434).
- * Windowed decoding changes the arithmetic: its parity gate is the BER curve, not bit-exactness.
- * Reference: the sub-block CUDA decoders ITTC/CUDA/turboDecoder.cu:20-21,205-331.
+ * Decoding schedule of the handle (BASELINE config 5).  NULL or window = 0
+ * (the default) is the exact full-trellis schedule of log_map.cpp.  Otherwise each codeword's
+ * trellis is cut into floor(L/window) sub-blocks (the last also takes the remainder, e.g. the 3
+ * tail steps) decoded in parallel: a sub-block's alpha starts `overlap` steps early and its beta
+ * `overlap` steps late from equal metrics, or with nii = 1 from the metrics the neighbouring
+ * chain had there in the previous iteration (NII, turboDecoderBianJieZhi.cu:248,302-304,
+ * 312,397-400); concurrent = 1 runs both SISOs at once on the other's extrinsic of the previous
+ * iteration (turboDecoderBianJieZhi.cu:642-690) instead of the serial order; the extrinsic is
+ * multiplied by ext_scale (1 = none; 0.77 in the reference GPU decoders, :423-434).  Windowed
+ * decoding changes the arithmetic: its gate is the BER curve, not bit-exactness.
+ *   the reference GPU decoder with P sub-blocks: {6144/P, 0, 1, 1, 0.77}, TD_ALGO_MAXLOG, TD_F32
  */
-int td_set_window(td_handle* h, int window, int overlap, float ext_scale);
+typedef struct td_window_params {
+    int window;        /* sub-block length W (0 = exact schedule) */
+    int overlap;       /* warm-up steps, 0 <= overlap <= 3*window */
+    int nii;           /* 1: boundary metrics from the previous iteration */
+    int concurrent;    /* 1: both SISOs concurrently (Jacobi) */
+    double ext_scale;  /* extrinsic scale, (0, 4] */
+} td_window_params;
+int td_set_window(td_handle* h, const td_window_params* w);
 
 /* Kernel timing (measurement support): while enabled, hipEvents on the decode stream bracket
  * the demultiplex kernel and the turbo kernel of every td_decode_device call.

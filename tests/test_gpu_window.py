@@ -6,6 +6,9 @@ pin the kernel's indexing first:
     Max-Log-MAP decoder IS the exact one (max is order-free): bits equal the oracle's, Le
     within 1e-9;
   * the single-sub-block case (L <= 64) likewise, at overlap 0.
+and every schedule option (sub-block length, overlap, NII boundaries, concurrent SISOs, extrinsic
+scale) is checked in Max-Log-MAP against oracle/window_oracle.py, a restatement of the
+reference's sub-block GPU decoder (ITTC/CUDA/turboDecoderBianJieZhi.cu).
 Then the BER of the windowed log-MAP decoder at K=6144 is compared with the exact schedule on
 the same generator frames."""
 import numpy as np
@@ -16,7 +19,8 @@ import pyoracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _decode(K, f1, f2, iters, flow, algo, window, overlap, precision="f64", ext_scale=1.0):
+def _decode(K, f1, f2, iters, flow, algo, window, overlap, precision="f64", ext_scale=1.0, nii=False,
+            concurrent=False):
     import torch
 
     from turbo_decoder_cuda_amd import TurboCodec
@@ -24,7 +28,7 @@ def _decode(K, f1, f2, iters, flow, algo, window, overlap, precision="f64", ext_
     x = torch.from_numpy(flow).to("cuda:0").to(dt).contiguous()
     B = flow.shape[0]
     with TurboCodec(K, f1, f2, iterations=iters, algo=algo, precision=precision) as c:
-        c.set_window(window, overlap, ext_scale)
+        c.set_window(window, overlap, ext_scale, nii=nii, concurrent=concurrent)
         bits = torch.empty((B, iters, K), dtype=torch.uint8, device=x.device)
         le = torch.empty((B, iters, 2, K + 3), dtype=dt, device=x.device)
         c.decode(x, bits, all_iters=True, le=le)
@@ -42,6 +46,26 @@ def test_window_maxlog_full_overlap_is_exact(K, f1, f2, B, overlap):
         ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=O.ALGO_MAXLOG)
         assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+
+
+@pytest.mark.parametrize("K,f1,f2,W,g,nii,conc,scale", [
+    (200, 13, 50, 48, 0, True, True, 0.77),      # the reference GPU decoder's schedule
+    (200, 13, 50, 64, 0, True, False, 1.0),
+    (200, 13, 50, 48, 6, False, True, 1.0),
+    (200, 13, 50, 50, 9, True, True, 0.77),      # W not a multiple of 3, overlap with NII
+    (512, 31, 64, 96, 30, True, False, 0.77),
+    (160, 21, 120, 64, 192, True, True, 1.0),    # overlap beyond both ends
+    (40, 3, 10, 16, 0, True, True, 0.5),
+])
+def test_window_schedules_vs_restatement(K, f1, f2, W, g, nii, conc, scale):
+    import window_oracle as WO
+    B, iters = 9, 5
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 11 + W + g, B)
+    bits, le = _decode(K, f1, f2, iters, flow, "maxlog", W, g, ext_scale=scale, nii=nii, concurrent=conc)
+    for b in range(B):
+        ob, ol = WO.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, nii=nii, concurrent=conc, scale=scale)
+        assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+        assert np.array_equal(bits[b], ob), f"codeword {b}"
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -81,7 +105,7 @@ def test_set_window_rejects_bad_arguments():
     from turbo_decoder_cuda_amd import TurboCodec
     from turbo_decoder_cuda_amd import _native as N
     with TurboCodec(1024, 31, 64, iterations=2) as c:
-        for w, g, s in ((32, 30, 1.0), (64, 31, 1.0), (64, -3, 1.0), (64, 195, 1.0), (64, 30, 0.0)):
+        for w, g, s in ((2, 0, 1.0), (64, -3, 1.0), (64, 195, 1.0), (64, 30, 0.0), (64, 30, 5.0)):
             with pytest.raises(N.TurboError):
                 c.set_window(w, g, s)
         c.set_window(0, 0, 1.0)

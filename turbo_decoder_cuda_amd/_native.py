@@ -32,6 +32,11 @@ class TdParams(C.Structure):
     ]
 
 
+class TdWindowParams(C.Structure):
+    _fields_ = [("window", C.c_int), ("overlap", C.c_int), ("nii", C.c_int), ("concurrent", C.c_int),
+                ("ext_scale", C.c_double)]
+
+
 class TurboError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"turbo_mi355x error {code}: {msg}")
@@ -79,7 +84,7 @@ def lib() -> C.CDLL:
     L.td_synth_seek.argtypes = [P, C.c_ulonglong]
     L.td_synth_frames.argtypes = [P, C.c_double, I, P, P, P]
     L.td_count_errors.argtypes = [P, P, I, P, I, P, P]
-    L.td_set_window.argtypes = [P, I, I, C.c_float]
+    L.td_set_window.argtypes = [P, C.POINTER(TdWindowParams)]
     _lib = L
     return L
 

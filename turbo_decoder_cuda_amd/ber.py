@@ -64,7 +64,7 @@ def ber_point(codec: TurboCodec, ebn0_db: float, max_frames: int, min_block_erro
             for it in range(iters):
                 pt.bit_errors[it] += int(err[b, it])
                 pt.block_errors[it] += int(err[b, it] != 0)
-            if pt.block_errors[stop_it] >= min_block_errors:
+            if min_block_errors > 0 and pt.block_errors[stop_it] >= min_block_errors:
                 done = True
                 break
     codec.synth_seek(start + pt.frames)   # the stream continues right after the last counted frame
@@ -137,11 +137,19 @@ def main(argv=None):
     ap.add_argument("--ebn0", type=float, nargs=3, default=[0.0, 1.0, 0.1], metavar=("START", "END", "STEP"))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-frames", type=int, default=100000)
-    ap.add_argument("--min-block-errors", type=int, default=50)
+    ap.add_argument("--min-block-errors", type=int, default=50, help="<= 0: decode max-frames per point")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--window", type=int, default=0, help="sub-block length (0 = exact schedule)")
+    ap.add_argument("--overlap", type=int, default=0)
+    ap.add_argument("--nii", action="store_true")
+    ap.add_argument("--concurrent", action="store_true")
+    ap.add_argument("--ext-scale", type=float, default=1.0)
+    ap.add_argument("--reference-gpu", type=int, default=0, metavar="P",
+                    help="the reference GPU decoder with P sub-blocks (turboDecoderBianJieZhi.cu): "
+                         "Max-Log-MAP fp32, window K/P, NII, concurrent SISOs, extrinsic x0.77")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     start, end, step = a.ebn0
@@ -149,7 +157,12 @@ def main(argv=None):
     while e <= end:   # main.cpp:172 accumulates the Eb/N0 (and so its sigma) exactly this way
         pts.append(e)
         e += step
+    if a.reference_gpu:
+        a.algo, a.precision = "maxlog", "f32"
+        a.window, a.overlap, a.nii, a.concurrent, a.ext_scale = a.K // a.reference_gpu, 0, True, True, 0.77
     with TurboCodec(a.K, a.f1, a.f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=a.device) as c:
+        if a.window:
+            c.set_window(a.window, a.overlap, a.ext_scale, nii=a.nii, concurrent=a.concurrent)
         res = ber_sweep(c, pts, a.seed, a.max_frames, a.min_block_errors, a.batch,
                         log=lambda s: print(s, file=sys.stderr, flush=True))
     for p in res:

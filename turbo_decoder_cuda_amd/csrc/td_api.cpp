@@ -66,9 +66,10 @@ struct td_handle {
     unsigned long long lfg_frames = 0;
     uint32_t* d_win = nullptr;
     int win_cap = 0;
-    // decoding schedule (td_set_window): 0 = exact full trellis
-    int window = 0;
-    td::WindowParams wp{0, 1.0f};
+    // decoding schedule (td_set_window): window 0 = exact full trellis
+    td::WindowParams wp{0, 0, 0, 0, 1.0f};
+    void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
+    size_t wws_bytes = 0;
 };
 
 namespace td {
@@ -180,6 +181,43 @@ int groups_for(int B)
     return ((B + 8 * gw - 1) / (8 * gw)) * gw;   // groups of 8 codewords, whole workgroups
 }
 
+// sub-blocks per codeword of the windowed schedule (the last also takes L mod W)
+int window_subblocks(int L, int W) { return L / W > 0 ? L / W : 1; }
+
+// the windowed schedule's buffers: the workspace's extrinsic pair and alpha scratch, plus a second
+// extrinsic pair and alpha scratch (concurrent schedule) and the NII metrics
+// [2 parity][2 dec][B][nS][2][8], grown on demand
+template <typename T>
+int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& wb)
+{
+    const size_t arrK = align_up((size_t)dp.G * dp.K * 8 * sizeof(T), 256);
+    const size_t nii = (size_t)2 * 2 * dp.G * 8 * window_subblocks(dp.L, h->wp.window) * 16 * sizeof(T);
+    const size_t arrA = h->wp.concurrent ? align_up((size_t)dp.G * dp.L * 64 * sizeof(T), 256) : 0;
+    const size_t need = 2 * arrK + arrA + nii;
+    if (need > h->wws_bytes) {
+        if (h->d_wws) {
+            TD_HIP(hipDeviceSynchronize());
+            TD_HIP(hipFree(h->d_wws));
+            h->d_wws = nullptr;
+            h->wws_bytes = 0;
+        }
+        if (hipMalloc(&h->d_wws, need) != hipSuccess) {
+            h->d_wws = nullptr;
+            return fail(TD_ENOMEM, "hipMalloc of the windowed-schedule buffers failed (" + std::to_string(need) + " B)");
+        }
+        h->wws_bytes = need;
+    }
+    char* w = static_cast<char*>(h->d_wws);
+    wb.ext12[0] = dp.ext12;
+    wb.ext21[0] = dp.ext21;
+    wb.ext12[1] = reinterpret_cast<T*>(w);
+    wb.ext21[1] = reinterpret_cast<T*>(w + arrK);
+    wb.astore[0] = dp.astore;
+    wb.astore[1] = h->wp.concurrent ? reinterpret_cast<T*>(w + 2 * arrK) : dp.astore;   // the SISOs overlap
+    wb.nii = reinterpret_cast<T*>(w + 2 * arrK + arrA);
+    return TD_OK;
+}
+
 template <typename T>
 int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                     hipStream_t st)
@@ -225,8 +263,15 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     hipError_t e = td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
-    e = h->window ? td::launch_window<T>(dp, h->wp, st) : td::launch_turbo<T>(dp, st);
-    if (e != hipSuccess) return hip_fail(e, h->window ? "launch_window" : "launch_turbo");
+    if (h->wp.window) {
+        td::WindowBufs<T> wb{};
+        rc = window_bufs<T>(h, dp, wb);
+        if (rc) return rc;
+        e = td::launch_window<T>(dp, h->wp, wb, st);
+    } else {
+        e = td::launch_turbo<T>(dp, st);
+    }
+    if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
     if (ev) TD_HIP(hipEventRecord(ev[2], st));
     return TD_OK;
 }
@@ -480,6 +525,7 @@ int td_destroy(td_handle* h)
     if (h->d_lut) (void)hipFree(h->d_lut);
     if (h->d_lane) (void)hipFree(h->d_lane);
     if (h->d_win) (void)hipFree(h->d_win);
+    if (h->d_wws) (void)hipFree(h->d_wws);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     delete h;
@@ -503,16 +549,19 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
     return decode_device_t<float>(h, d_llr, B, d_bits, all_iters, d_le, st);
 }
 
-int td_set_window(td_handle* h, int window, int overlap, float ext_scale)
+int td_set_window(td_handle* h, const td_window_params* w)
 {
     if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
-    if (window != 0 && window != td::sliding_window_steps())
-        return fail(TD_EINVAL, "td_set_window: window must be 0 (exact) or " + std::to_string(td::sliding_window_steps()));
-    if (overlap < 0 || overlap > 3 * td::sliding_window_steps() || overlap % 3)
-        return fail(TD_EINVAL, "td_set_window: overlap must be a multiple of 3 in [0, 3*window]");
-    if (!(ext_scale > 0.0f) || !(ext_scale <= 4.0f)) return fail(TD_EINVAL, "td_set_window: ext_scale must be in (0, 4]");
-    h->window = window;
-    h->wp = td::WindowParams{overlap, ext_scale};
+    if (!w || w->window == 0) {
+        h->wp = td::WindowParams{0, 0, 0, 0, 1.0f};
+        return TD_OK;
+    }
+    if (w->window < 3 || w->window > 10000) return fail(TD_EINVAL, "td_set_window: window must be 0 or in [3, 10000]");
+    if (w->overlap < 0 || w->overlap > 3 * w->window)
+        return fail(TD_EINVAL, "td_set_window: overlap must be in [0, 3*window]");
+    if (!(w->ext_scale > 0.0) || !(w->ext_scale <= 4.0))
+        return fail(TD_EINVAL, "td_set_window: ext_scale must be in (0, 4]");
+    h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale};
     return TD_OK;
 }
 

@@ -60,13 +60,24 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 template <typename T>
 hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st);
 
-// sliding-window mode (BASELINE config 5): sub-blocks of 64 steps with `overlap` warm-up steps
+// sliding-window mode (BASELINE config 5, td_set_window): sub-blocks of `window` steps
 struct WindowParams {
-    int overlap;       // warm-up steps (multiple of 3)
-    float ext_scale;   // extrinsic scaling (1 = none)
+    int window;        // sub-block length W (the last sub-block also takes L mod W)
+    int overlap;       // warm-up steps g
+    int nii;           // boundary metrics from the previous iteration
+    int concurrent;    // both SISOs per launch on the previous iteration's extrinsics
+    double ext_scale;  // extrinsic scaling (1 = none)
+};
+// extra device buffers of the windowed schedule
+template <typename T>
+struct WindowBufs {
+    T* ext12[2];   // [G][K][8] x2 (concurrent schedule: iteration parity); serial uses [0]
+    T* ext21[2];
+    T* nii;        // [2 parity][2 dec][B][nS][2][8]
+    T* astore[2];  // per decoder alpha scratch [G][L][64] (concurrent: two; serial: one)
 };
 template <typename T>
-hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st);
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st);
 
 template <typename T>
 hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* la_ws, int terminated, T* llr,
@@ -86,7 +97,6 @@ hipError_t launch_count_errors(const uint8_t* bits, const uint8_t* info, int K, 
                                hipStream_t st);
 
 int window_steps();
-int sliding_window_steps();   // sub-block length of launch_window (64)
 int groups_per_wg();   // codeword groups (of 8) per workgroup: G must be a multiple of this
 
 }  // namespace td

@@ -918,24 +918,40 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
 }
 
 // ================================================================== sliding-window mode
-// BASELINE config 5 / SURVEY.md 8f row 3: the trellis of each codeword is cut into sub-blocks of
-// W steps decoded in parallel.  A sub-block's alpha starts g steps early from equal metrics
-// (overlap initialisation) and its beta g steps late; only the codeword's first alpha and last
-// beta start from the true initial / terminated states.  Each 8-lane group of a wave holds one
-// (codeword, sub-block) pair, so a wave runs 8 independent chains and thousands of waves are in
-// flight: this mode is throughput-bound, not latency-bound.  It is NOT the reference's
-// arithmetic: the windows' boundary metrics are approximations, the LLR fold is a butterfly (tree
-// order) max*, and the extrinsic may be scaled (ext_scale).  The SISO schedule is the
-// reference's serial one (one launch per SISO).
+// BASELINE config 5 / SURVEY.md 8f row 3: the trellis of each codeword is cut into nS sub-blocks
+// of W steps (the last one also takes the remainder, e.g. the 3 tail steps) decoded in parallel.
+// A sub-block's alpha starts g steps early and its beta g steps late (overlap warm-up), from
+//   * equal metrics, or
+//   * NII (next-iteration initialisation): the metrics the neighbouring sub-block's chain had at
+//     that position in the previous iteration (ITTC/CUDA/turboDecoderBianJieZhi.cu:248,302-304,
+//     312,397-400 -- g = 0 there);
+// only the codeword's first alpha and last beta start from the true initial / terminated states.
+// The SISOs run in the reference's serial order (one launch per SISO) or concurrently (both in one
+// launch, each using the other's extrinsic of the previous iteration: turboDecoderBianJieZhi.cu
+// :642-690), and the extrinsic may be scaled (0.77 there, :423-434).  Each 8-lane group of a wave
+// holds one (decoder, codeword, sub-block) task, so a wave runs 8 independent chains and
+// thousands of waves are in flight: this mode is throughput-bound, not latency-bound.  It is not
+// the reference CPU decoder's arithmetic (window boundaries, butterfly-order LLR fold), so its gate
+// is the BER curve.
 //
 // Labels rotate with the step index relative to the chain's origin i0 = s*W - g (the trellis is
 // time-invariant), so the 8 groups of a wave stay in phase whatever their absolute steps; slot 0
-// holds state 0 at every phase.
+// holds state 0 at every phase, so the true initial / terminated metrics are phase-free.  Metrics
+// that cross tasks (the alpha scratch, NII boundaries) are stored by state.
+template <typename T>
 struct WinArgs {
-    int W, g;          // sub-block length, overlap
-    int nS;            // sub-blocks per codeword
-    float ext_scale;
-    int dec, it;       // SISO 0/1, iteration
+    int W, g;              // sub-block length, overlap
+    int nS;                // sub-blocks per codeword (the last is L - (nS-1)W long, W..2W-1)
+    T ext_scale;
+    int dec;               // serial: this launch's SISO; -1: both (concurrent schedule)
+    int it;                // iteration
+    int la_len;            // La valid for steps < la_len (0 before any extrinsic exists)
+    int nii;               // boundary metrics from nii_rd (after the first iteration)
+    const T* la[2];        // per decoder: La [G][K][8] (dec 0 natural order, dec 1 interleaved)
+    T* le[2];              // per decoder: Le out, scattered to the other decoder's order
+    const T* nii_rd;       // [2 dec][B][nS][2][8]: alpha (0) / beta (1) at the chain's start
+    T* nii_wr;
+    T* astore[2];          // per decoder alpha scratch [G][L][64]
 };
 
 template <typename T>
@@ -945,20 +961,20 @@ struct SwIn {
 
 // channel + a-priori of (codeword b, step i) for decoder `dec` (steps outside [0, L) clamped)
 template <typename T>
-__device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, int dec, int la_len, int b, int i)
+__device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
 {
     const int ic = min(max(i, 0), p.L - 1);
     const size_t off = ((size_t)(b >> 3) * p.L + ic) * kCw + (b & 7);
     const T ys = (dec ? p.sys2 : p.sys1)[off];
     const T yp = (dec ? p.par2 : p.par1)[off];
-    const T* la_arr = dec ? p.ext12 : p.ext21;
-    const T lr = la_arr[((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
-    const T la = ic < la_len ? lr : (T)0;
+    const T lr = a.la[dec][((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
+    const T la = ic < a.la_len ? lr : (T)0;
     const T hla = la / (T)2;
     return SwIn<T>{(ys + yp) + hla, (ys - yp) + hla, ys, la};
 }
 
-// one alpha step of phase PH on a group's metric (normalised by the group max); `freeze` keeps it
+// one alpha / beta step of phase PH on a group's metric (normalised by the group max);
+// `freeze` keeps the metric
 template <typename T, int ALGO, int PH>
 __device__ __forceinline__ T sw_alpha_step(T alpha, const SwIn<T>& in, const T* lut, const LaneConst<T>& lc, bool freeze)
 {
@@ -990,54 +1006,80 @@ __device__ __forceinline__ T sw_group_mstar(T v, const T* lut)
 }
 
 template <typename T>
-struct SwCtx {
-    const DecodeParams<T>& p;
-    const WinArgs& a;
-    const LaneConst<T>& lc;
-    const T* lut;
-    int b, s, la_len, i0;
+struct SwTask {
+    int dec, b, s;
+    int i0;         // absolute step of relative index 0 (s*W - g)
+    int len;        // steps of this sub-block
     bool live;
     int slot;
-    bool want_bits;
+    int soff;       // (b & 7) * 8 - (lane & ~7): lane's st_off -> alpha scratch column of codeword b
+    size_t nii;     // ((dec * B + b) * nS + s) * 16: this task's NII slots
 };
 
-// beta step at relative index kr (absolute i = i0 + kr, phase PH = kr % 3), with the LLR fold of
-// step i when i lies in the sub-block: the lane's two LLR terms belong to the next state its
-// beta[.][i+1] is held for (the alpha step's self / partner transitions)
-template <typename T, int ALGO, int PH, int W>
-__device__ __forceinline__ T sw_beta_fold(const SwCtx<T>& cx, T beta, int kr)
+// alpha chain position k (relative): store alpha[.][i0+k] (by state) if it lies in the
+// sub-block, save it as the NII alpha of sub-block s+1 at k = W, then step (k < n)
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T sw_alpha_at(const DecodeParams<T>& p, const WinArgs<T>& a, const SwTask<T>& t,
+                                         const LaneConst<T>& lc, const T* lut, T alpha, int k, int n)
 {
-    const DecodeParams<T>& p = cx.p;
-    const LaneConst<T>& lc = cx.lc;
-    const int i = cx.i0 + kr;
-    const SwIn<T> x = sw_load(p, cx.a.dec, cx.la_len, cx.b, i);
-    if (kr < cx.a.g + W && i < p.L) {
-        const T al = p.astore[((size_t)(cx.b >> 3) * p.L + i) * kLanes + (cx.b & 7) * 8 + lc.st_off[PH] - (threadIdx.x & 56)];
+    const int i = t.i0 + k;
+    if (t.live && i >= t.i0 + a.g && i < t.i0 + a.g + t.len && i < p.L)
+        a.astore[t.dec][((size_t)(t.b >> 3) * p.L + i) * kLanes + lc.st_off[PH] + t.soff] = alpha;
+    if (t.live && k == a.W && t.s < a.nS - 1)
+        a.nii_wr[t.nii + 16 + (lc.st_off[PH] & 7)] = alpha;   // alpha slot of task s+1
+    if (k < n) alpha = sw_alpha_step<T, ALGO, PH>(alpha, sw_load(p, a, t.dec, t.b, i), lut, lc, i < 0);
+    return alpha;
+}
+
+// beta chain at relative index kr (phase PH): start the task's chain at its top, fold step
+// i = i0 + kr when it lies in the sub-block (alpha[.][i] from the scratch, beta[.][i+1] held:
+// the lane's two LLR terms are the alpha step's self / partner transitions into the state its
+// beta is held for), step, and save beta[.][i0+2g] as the NII beta of sub-block s-1
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T sw_beta_at(const DecodeParams<T>& p, const WinArgs<T>& a, const SwTask<T>& t,
+                                        const LaneConst<T>& lc, const T* lut, T beta, int kr, bool want_bits)
+{
+    const int top = t.len + 2 * a.g - 1;
+    if (kr > top) return beta;
+    const int i = t.i0 + kr;
+    if (kr == top) {   // beta[.][i+1] (labels of phase PH+1)
+        if (i + 1 >= p.L)
+            beta = t.slot == 0 ? (T)0 : (T)-kInfty;
+        else if (a.nii && a.it > 0)
+            beta = a.nii_rd[t.nii + 8 + (lc.st_off[(PH + 1) % 3] & 7)];
+        else
+            beta = (T)0;
+    }
+    const SwIn<T> x = sw_load(p, a, t.dec, t.b, i);
+    if (kr < a.g + t.len && i < p.L) {
+        const T al = a.astore[t.dec][((size_t)(t.b >> 3) * p.L + i) * kLanes + lc.st_off[PH] + t.soff];
         const T gs = lc.a_sel[PH] ? x.Q : x.P, gp = lc.a_psel[PH] ? x.Q : x.P;
         const T alp = dpp<PhaseDpp<PH>::ctrl>(al);
         const T xs = fma(lc.a_sg[PH], gs, al) + beta, xp = fma(lc.a_pg[PH], gp, alp) + beta;
         const bool us = lc.a_sg[PH] > (T)0;
-        const T m1 = sw_group_mstar<T, ALGO>(us ? xs : xp, cx.lut), m0 = sw_group_mstar<T, ALGO>(us ? xp : xs, cx.lut);
+        const T m1 = sw_group_mstar<T, ALGO>(us ? xs : xp, lut), m0 = sw_group_mstar<T, ALGO>(us ? xp : xs, lut);
         const T llr = m1 - m0;
-        if (cx.live && cx.slot == 0) {
-            const T le = (llr - x.la - (T)2 * x.ys) * (T)cx.a.ext_scale;
-            const int c = cx.b & 7, g8 = cx.b >> 3;
+        if (t.live && t.slot == 0) {
+            const T le = (llr - x.la - (T)2 * x.ys) * a.ext_scale;
+            const int c = t.b & 7, g8 = t.b >> 3;
             if (i < p.K) {
-                const int w = cx.a.dec ? p.pi[i] : p.pinv[i];
-                T* ext = cx.a.dec ? p.ext21 : p.ext12;
-                ext[((size_t)g8 * p.K + w) * kCw + c] = le;
-                if (cx.want_bits)
-                    p.bits[(size_t)cx.b * (p.all_iters ? p.iters * p.K : p.K) +
-                           (size_t)(p.all_iters ? cx.a.it : 0) * p.K + p.pi[i]] = llr < (T)0 ? 0 : 1;
+                const int w = t.dec ? p.pi[i] : p.pinv[i];
+                a.le[t.dec][((size_t)g8 * p.K + w) * kCw + c] = le;
+                if (want_bits)
+                    p.bits[(size_t)t.b * (p.all_iters ? p.iters * p.K : p.K) + (size_t)(p.all_iters ? a.it : 0) * p.K +
+                           p.pi[i]] = llr < (T)0 ? 0 : 1;
             }
-            if (p.le_dump) p.le_dump[(size_t)cx.b * p.iters * 2 * p.L + (size_t)(2 * cx.a.it + cx.a.dec) * p.L + i] = le;
+            if (p.le_dump) p.le_dump[(size_t)t.b * p.iters * 2 * p.L + (size_t)(2 * a.it + t.dec) * p.L + i] = le;
         }
     }
-    return sw_beta_step<T, ALGO, PH>(beta, x, cx.lut, lc, i + 1 > p.L);   // beyond the end: hold the init
+    beta = sw_beta_step<T, ALGO, PH>(beta, x, lut, lc, i + 1 > p.L);   // beyond the end: hold the init
+    if (t.live && kr == 2 * a.g && t.s > 0)
+        a.nii_wr[t.nii - 16 + 8 + (lc.st_off[PH] & 7)] = beta;        // beta slot of task s-1
+    return beta;
 }
 
-template <typename T, int ALGO, int W>
-__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs a)
+template <typename T, int ALGO>
+__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[2 * kLutRows * kLutCols];
     for (int e = threadIdx.x; e < kLutRows * kLutCols; e += blockDim.x) {
@@ -1047,75 +1089,101 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
         lut_s[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, slot = lane & 7;
+    const int lane = threadIdx.x & 63;
     const T* lut = lut_s + (lane % kLutCols);
     LaneConst<T> lc;
     lane_setup(p.lane, lane, lc);
+    const int per_dec = p.B * a.nS;
     const int task = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (lane >> 3);
-    const bool live = task < p.B * a.nS;
-    const int b = live ? task / a.nS : 0, s = live ? task % a.nS : 0;
-    const int la_len = (a.dec == 0 && a.it == 0) ? 0 : p.K;
-    const int i0 = s * W - a.g;   // absolute step of relative index 0
+    SwTask<T> t;
+    t.live = task < (a.dec < 0 ? 2 : 1) * per_dec;
+    const int tk = t.live ? task : 0;
+    t.dec = a.dec < 0 ? tk / per_dec : a.dec;
+    t.b = (tk % per_dec) / a.nS;
+    t.s = tk % a.nS;
+    t.i0 = t.s * a.W - a.g;
+    t.len = t.s == a.nS - 1 ? p.L - t.s * a.W : a.W;
+    t.slot = lane & 7;
+    t.soff = (t.b & 7) * 8 - (lane & ~7);
+    t.nii = (((size_t)t.dec * p.B + t.b) * a.nS + t.s) * 16;
+    const int wmax = p.L - (a.nS - 1) * a.W;   // the longest sub-block (uniform loop bounds)
 
-    // ---- alpha: g warm-up steps then the W steps of the sub-block, stored by state in the
-    // alpha scratch ([G][L][64], L2-resident between the two passes)
-    const T init = slot == 0 ? (T)0 : (T)-kInfty;
-    T alpha = i0 <= 0 ? init : (T)0;   // i0 <= 0: the chain reaches (or starts at) step 0
-    T* arow = p.astore + ((size_t)(b >> 3) * p.L) * kLanes + (b & 7) * 8;
-    for (int k = 0; k + 3 <= a.g + W; k += 3) {   // g + W = 0 mod 3 is not required: tail below
-        const int i = i0 + k;
-        const SwIn<T> x0 = sw_load(p, a.dec, la_len, b, i), x1 = sw_load(p, a.dec, la_len, b, i + 1),
-                      x2 = sw_load(p, a.dec, la_len, b, i + 2);
-        if (live && i >= s * W && i < p.L) arow[(size_t)i * kLanes + lc.st_off[0] - (lane & ~7)] = alpha;
-        alpha = sw_alpha_step<T, ALGO, 0>(alpha, x0, lut, lc, i < 0);
-        if (live && i + 1 >= s * W && i + 1 < p.L) arow[(size_t)(i + 1) * kLanes + lc.st_off[1] - (lane & ~7)] = alpha;
-        alpha = sw_alpha_step<T, ALGO, 1>(alpha, x1, lut, lc, i + 1 < 0);
-        if (live && i + 2 >= s * W && i + 2 < p.L) arow[(size_t)(i + 2) * kLanes + lc.st_off[2] - (lane & ~7)] = alpha;
-        alpha = sw_alpha_step<T, ALGO, 2>(alpha, x2, lut, lc, i + 2 < 0);
-    }
-    {   // W = 64 = 1 mod 3: the last stored step (phase 0)
-        const int i = i0 + ((a.g + W) / 3) * 3;
-        if (live && i >= s * W && i < p.L && i < s * W + W) arow[(size_t)i * kLanes + lc.st_off[0] - (lane & ~7)] = alpha;
+    // ---- alpha: g warm-up steps, then the sub-block's steps stored by state in the alpha
+    // scratch ([G][L][64]); chains of shorter sub-blocks run on past their end unstored
+    T alpha;
+    if (t.i0 <= 0)
+        alpha = t.slot == 0 ? (T)0 : (T)-kInfty;   // the chain reaches (or starts at) step 0
+    else if (a.nii && a.it > 0)
+        alpha = a.nii_rd[t.nii + (lc.st_off[0] & 7)];
+    else
+        alpha = (T)0;
+    const int n = a.g + wmax;
+    for (int k = 0; k <= n; k += 3) {
+        alpha = sw_alpha_at<T, ALGO, 0>(p, a, t, lc, lut, alpha, k, n);
+        if (k + 1 > n) break;
+        alpha = sw_alpha_at<T, ALGO, 1>(p, a, t, lc, lut, alpha, k + 1, n);
+        if (k + 2 > n) break;
+        alpha = sw_alpha_at<T, ALGO, 2>(p, a, t, lc, lut, alpha, k + 2, n);
     }
 
-    // ---- beta: g warm-up steps down to the sub-block's end, then the W steps with the LLR fold;
-    // relative index kr = i - i0 from W + 2g - 1 (= 0 mod 3) down to g, phases 0, 2, 1, ...
-    const int e_end = s * W + W + a.g;   // absolute index of the first beta (beta[.][e_end])
-    T beta = e_end >= p.L ? init : (T)0;
-    SwCtx<T> cx{p, a, lc, lut, b, s, la_len, i0, live, slot, a.dec == 1 && (p.all_iters || a.it == p.iters - 1)};
-    int kr = W + 2 * a.g - 1;
-    for (; kr - 2 >= a.g; kr -= 3) {
-        beta = sw_beta_fold<T, ALGO, 0, W>(cx, beta, kr);
-        beta = sw_beta_fold<T, ALGO, 2, W>(cx, beta, kr - 1);
-        beta = sw_beta_fold<T, ALGO, 1, W>(cx, beta, kr - 2);
+    // ---- beta: from relative index wmax + 2g - 1 down to g (tasks start at their own top)
+    const bool want_bits = t.dec == 1 && (p.all_iters || a.it == p.iters - 1);
+    T beta = (T)0;
+    for (int kr = wmax + 2 * a.g - 1; kr >= a.g; --kr) {
+        switch (kr % 3) {   // wave-uniform
+            case 0: beta = sw_beta_at<T, ALGO, 0>(p, a, t, lc, lut, beta, kr, want_bits); break;
+            case 1: beta = sw_beta_at<T, ALGO, 1>(p, a, t, lc, lut, beta, kr, want_bits); break;
+            default: beta = sw_beta_at<T, ALGO, 2>(p, a, t, lc, lut, beta, kr, want_bits); break;
+        }
     }
-    if (kr >= a.g) beta = sw_beta_fold<T, ALGO, 0, W>(cx, beta, kr);   // W + g = 1 mod 3: one step left
 }
 
-constexpr int kSwW = 64;   // compiled sub-block length (BASELINE config 5)
-
 template <typename T, int ALGO>
-hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st)
+hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)
 {
-    const int nS = (p.L + kSwW - 1) / kSwW;
-    const long long tasks = (long long)p.B * nS;
-    const int blocks = (int)((tasks + 31) / 32);   // 4 waves x 8 groups per block
-    for (int it = 0; it < p.iters; ++it)
-        for (int dec = 0; dec < 2; ++dec) {
-            WinArgs a{kSwW, w.overlap, nS, w.ext_scale, dec, it};
-            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO, kSwW>), dim3(blocks), dim3(256), 0, st, p, a);
+    const int W = w.window;
+    const int nS = p.L / W > 0 ? p.L / W : 1;
+    WinArgs<T> a{};
+    a.W = W;
+    a.g = w.overlap;
+    a.nS = nS;
+    a.ext_scale = (T)w.ext_scale;
+    a.nii = w.nii;
+    a.astore[0] = wb.astore[0];
+    a.astore[1] = wb.astore[1];
+    const size_t nii_half = (size_t)2 * p.B * nS * 16;
+    for (int it = 0; it < p.iters; ++it) {
+        a.it = it;
+        a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
+        a.nii_wr = wb.nii + (size_t)(it & 1) * nii_half;
+        for (int dec = 0; dec < (w.concurrent ? 1 : 2); ++dec) {
+            if (w.concurrent) {   // Jacobi: both SISOs read the other's Le of iteration it-1
+                a.dec = -1;
+                a.la_len = it == 0 ? 0 : p.K;
+                a.la[0] = wb.ext21[(it + 1) & 1];
+                a.la[1] = wb.ext12[(it + 1) & 1];
+                a.le[0] = wb.ext12[it & 1];
+                a.le[1] = wb.ext21[it & 1];
+            } else {
+                a.dec = dec;
+                a.la_len = (it == 0 && dec == 0) ? 0 : p.K;
+                a.la[0] = a.le[1] = wb.ext21[0];
+                a.la[1] = a.le[0] = wb.ext12[0];
+            }
+            const long long tasks = (long long)p.B * nS * (w.concurrent ? 2 : 1);
+            const int blocks = (int)((tasks + 31) / 32);   // 4 waves x 8 tasks per block
+            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO>), dim3(blocks), dim3(256), 0, st, p, a);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
+    }
     return hipSuccess;
 }
 
-int sliding_window_steps() { return kSwW; }
-
 template <typename T>
-hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, hipStream_t st)
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)
 {
-    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, st) : launch_window_algo<T, 0>(p, w, st);
+    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st) : launch_window_algo<T, 0>(p, w, wb, st);
 }
 
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
@@ -1266,8 +1334,10 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t);
-template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, hipStream_t);
-template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, hipStream_t);
+template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, const WindowBufs<double>&,
+                                         hipStream_t);
+template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, const WindowBufs<float>&,
+                                        hipStream_t);
 template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);

@@ -66,9 +66,13 @@ class TurboCodec:
     def reserve(self, B: int) -> None:
         N.check(N.lib().td_reserve(self._h, int(B)))
 
-    def set_window(self, window: int = 64, overlap: int = 32 // 3 * 3, ext_scale: float = 1.0) -> None:
-        """Sliding-window schedule (td_set_window; BASELINE config 5). window=0: exact schedule."""
-        N.check(N.lib().td_set_window(self._h, int(window), int(overlap), float(ext_scale)))
+    def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
+                   concurrent: bool = False) -> None:
+        """Windowed schedule (td_set_window; BASELINE config 5); window=0: exact.
+        The reference GPU decoder with P sub-blocks (turboDecoderBianJieZhi.cu) is
+        set_window(6144 // P, 0, 0.77, nii=True, concurrent=True) on a maxlog / f32 codec."""
+        w = N.TdWindowParams(int(window), int(overlap), int(bool(nii)), int(bool(concurrent)), float(ext_scale))
+        N.check(N.lib().td_set_window(self._h, C.byref(w)))
         self.window = int(window)
 
     # -- TurboDecoding, host arrays ------------------------------------------------------
