@@ -109,3 +109,27 @@ def test_set_window_rejects_bad_arguments():
             with pytest.raises(N.TurboError):
                 c.set_window(w, g, s)
         c.set_window(0, 0, 1.0)
+
+
+def test_reference_gpu_decoder_ber_matches_published():
+    """The reference GPU decoder's schedule (P = 64 sub-blocks, NII, concurrent SISOs, Le x0.77,
+    Max-Log-MAP fp32) at 10 iterations on 2000 of main.cpp's frames per point: BER and FER
+    within 25% of the published 10000-frame values (tests/golden/psweep_published.json) at
+    0.4-0.6 dB, where both have thousands of bit errors.  The full sweep (all P, 25 iterations,
+    10000 frames) is scripts/psweep.py: profiles/r01/psweep_summary.txt."""
+    import json
+    import os
+
+    from conftest import GOLD
+    from turbo_decoder_cuda_amd import TurboCodec
+    from turbo_decoder_cuda_amd.ber import ber_point
+    pub = json.load(open(os.path.join(GOLD, "psweep_published.json")))["P"]["64"]
+    with TurboCodec(6144, 263, 480, iterations=10, algo="maxlog", precision="f32") as c:
+        c.set_window(96, 0, 0.77, nii=True, concurrent=True)
+        c.synth_seed(3)
+        for k in (4, 5, 6):
+            pt = ber_point(c, pub[k]["ebn0_db"], 2000, min_block_errors=0, batch=2000)
+            ber, fer = pt.ber[9], pt.bler[9]
+            print(pub[k]["ebn0_db"], ber, pub[k]["ber"][9], fer, pub[k]["fer"][9])
+            assert abs(ber / pub[k]["ber"][9] - 1) < 0.25
+            assert abs(fer / pub[k]["fer"][9] - 1) < 0.25

@@ -181,19 +181,17 @@ int groups_for(int B)
     return ((B + 8 * gw - 1) / (8 * gw)) * gw;   // groups of 8 codewords, whole workgroups
 }
 
-// sub-blocks per codeword of the windowed schedule (the last also takes L mod W)
-int window_subblocks(int L, int W) { return L / W > 0 ? L / W : 1; }
-
-// the windowed schedule's buffers: the workspace's extrinsic pair and alpha scratch, plus a second
-// extrinsic pair and alpha scratch (concurrent schedule) and the NII metrics
-// [2 parity][2 dec][B][nS][2][8], grown on demand
+// the windowed schedule's buffers: the workspace's extrinsic pair plus a second pair (concurrent
+// schedule), the alpha checkpoints of each decoder and the NII metrics [2 parity][2 dec][B][nS][2][8],
+// grown on demand
 template <typename T>
 int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& wb)
 {
     const size_t arrK = align_up((size_t)dp.G * dp.K * 8 * sizeof(T), 256);
-    const size_t nii = (size_t)2 * 2 * dp.G * 8 * window_subblocks(dp.L, h->wp.window) * 16 * sizeof(T);
-    const size_t arrA = h->wp.concurrent ? align_up((size_t)dp.G * dp.L * 64 * sizeof(T), 256) : 0;
-    const size_t need = 2 * arrK + arrA + nii;
+    const size_t nii = (size_t)2 * 2 * dp.B * td::window_subblocks(dp.L, h->wp.window) * 16 * sizeof(T);
+    const size_t arrC =
+        align_up(td::window_ckpt_elems(dp.B, dp.L, h->wp.window, sizeof(T) == 4) * sizeof(T), 256);
+    const size_t need = 2 * arrK + 2 * arrC + nii;
     if (need > h->wws_bytes) {
         if (h->d_wws) {
             TD_HIP(hipDeviceSynchronize());
@@ -212,9 +210,9 @@ int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& 
     wb.ext21[0] = dp.ext21;
     wb.ext12[1] = reinterpret_cast<T*>(w);
     wb.ext21[1] = reinterpret_cast<T*>(w + arrK);
-    wb.astore[0] = dp.astore;
-    wb.astore[1] = h->wp.concurrent ? reinterpret_cast<T*>(w + 2 * arrK) : dp.astore;   // the SISOs overlap
-    wb.nii = reinterpret_cast<T*>(w + 2 * arrK + arrA);
+    wb.ckpt[0] = reinterpret_cast<T*>(w + 2 * arrK);
+    wb.ckpt[1] = reinterpret_cast<T*>(w + 2 * arrK + arrC);   // the concurrent SISOs run together
+    wb.nii = reinterpret_cast<T*>(w + 2 * arrK + 2 * arrC);
     return TD_OK;
 }
 

@@ -74,8 +74,11 @@ struct WindowBufs {
     T* ext12[2];   // [G][K][8] x2 (concurrent schedule: iteration parity); serial uses [0]
     T* ext21[2];
     T* nii;        // [2 parity][2 dec][B][nS][2][8]
-    T* astore[2];  // per decoder alpha scratch [G][L][64] (concurrent: two; serial: one)
+    T* ckpt[2];    // per decoder alpha checkpoints (window_ckpt_elems; serial: one shared)
 };
+// sub-blocks per codeword (the last also takes L mod W) and the checkpoint scratch per decoder
+inline int window_subblocks(int L, int W) { return L / W > 0 ? L / W : 1; }
+size_t window_ckpt_elems(int B, int L, int W, bool f32);
 template <typename T>
 hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st);
 

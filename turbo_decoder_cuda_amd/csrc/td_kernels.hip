@@ -934,14 +934,20 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
 // the reference CPU decoder's arithmetic (window boundaries, butterfly-order LLR fold), so its gate
 // is the BER curve.
 //
-// Labels rotate with the step index relative to the chain's origin i0 = s*W - g (the trellis is
-// time-invariant), so the 8 groups of a wave stay in phase whatever their absolute steps; slot 0
-// holds state 0 at every phase, so the true initial / terminated metrics are phase-free.  Metrics
-// that cross tasks (the alpha scratch, NII boundaries) are stored by state.
+//
+// Layout: one lane per task with the 8 state metrics in registers (the per-state updates are
+// independent: 8-way ILP per lane, no cross-lane traffic), 64 tasks per wave = 64 consecutive
+// codewords of one (decoder, sub-block), so every wave runs the same chain lengths.  The alpha
+// pass keeps only a checkpoint every S steps (HBM scratch, lane-contiguous); the beta pass walks
+// the sub-block in segments of S steps: it loads the segment's inputs once, recomputes the
+// segment's alpha from its checkpoint into registers, then runs beta and the LLR fold backwards
+// over it.  HBM traffic per task-step: the inputs twice plus 8/S alpha values each way.
 template <typename T>
 struct WinArgs {
     int W, g;              // sub-block length, overlap
     int nS;                // sub-blocks per codeword (the last is L - (nS-1)W long, W..2W-1)
+    int Bp;                // codewords per (decoder, sub-block) rounded up to whole waves
+    int ncp;               // alpha checkpoints per task (ceil(longest sub-block / S))
     T ext_scale;
     int dec;               // serial: this launch's SISO; -1: both (concurrent schedule)
     int it;                // iteration
@@ -951,7 +957,7 @@ struct WinArgs {
     T* le[2];              // per decoder: Le out, scattered to the other decoder's order
     const T* nii_rd;       // [2 dec][B][nS][2][8]: alpha (0) / beta (1) at the chain's start
     T* nii_wr;
-    T* astore[2];          // per decoder alpha scratch [G][L][64]
+    T* ckpt[2];            // per decoder: [wave][ncp][8][64] alpha checkpoints
 };
 
 template <typename T>
@@ -959,7 +965,7 @@ struct SwIn {
     T P, Q, ys, la;
 };
 
-// channel + a-priori of (codeword b, step i) for decoder `dec` (steps outside [0, L) clamped)
+// channel + a-priori of (codeword b, step i) of decoder `dec` (steps outside [0, L) clamped)
 template <typename T>
 __device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
 {
@@ -973,184 +979,214 @@ __device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, const WinAr
     return SwIn<T>{(ys + yp) + hla, (ys - yp) + hla, ys, la};
 }
 
-// one alpha / beta step of phase PH on a group's metric (normalised by the group max);
-// `freeze` keeps the metric
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T sw_alpha_step(T alpha, const SwIn<T>& in, const T* lut, const LaneConst<T>& lc, bool freeze)
+// gamma of the transition leaving state s with input u: +-(P or Q), see "gamma"
+template <typename T>
+__device__ __forceinline__ T sw_g(const SwIn<T>& x, int s)
 {
-    const T gs = lc.a_sel[PH] ? in.Q : in.P, gp = lc.a_psel[PH] ? in.Q : in.P;
-    const T ap = dpp<PhaseDpp<PH>::ctrl>(alpha);
-    const T a = mstar<T, ALGO>(fma(lc.a_sg[PH], gs, alpha), fma(lc.a_pg[PH], gp, ap), lut);
-    const T m = group_max8(a);
-    return freeze ? alpha : a - m;
+    return kTrellisQ[s] ? x.Q : x.P;
 }
 
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T sw_beta_step(T beta, const SwIn<T>& in, const T* lut, const LaneConst<T>& lc, bool freeze)
-{
-    const T gs = lc.b_sel[PH] ? in.Q : in.P, gp = lc.b_psel[PH] ? in.Q : in.P;
-    const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
-    const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], gs, beta), fma(lc.b_pg[PH], gp, bp), lut);
-    const T m = group_max8(b);
-    return freeze ? beta : b - m;
-}
-
-// max* over the 8 lanes of a group, butterfly (every lane gets the tree result)
+// alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-1001), max-normalised
 template <typename T, int ALGO>
-__device__ __forceinline__ T sw_group_mstar(T v, const T* lut)
+__device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const T* lut)
 {
-    v = mstar<T, ALGO>(v, dpp<kDppXor1>(v), lut);
-    v = mstar<T, ALGO>(v, dpp<kDppXor2>(v), lut);
-    v = mstar<T, ALGO>(v, dpp<kDppMir8>(v), lut);
-    return v;
+    T n[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        n[j] = mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
+    }
+    const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = n[j] - m;
+}
+
+// beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1021), max-normalised
+template <typename T, int ALGO>
+__device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const T* lut)
+{
+    T n[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const T G = sw_g(x, j);
+        n[j] = mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
+    }
+    const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = n[j] - m;
+}
+
+// LLR of step i (log_map.cpp:1024-1039): the two left folds of E over the 8 next states
+template <typename T, int ALGO>
+__device__ __forceinline__ T sw_llr(const T (&a)[8], const T (&b)[8], const SwIn<T>& x, const T* lut)
+{
+    T t0[8], t1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        t0[j] = (a[p0] - sw_g(x, p0)) + b[j];
+        t1[j] = (a[p1] + sw_g(x, p1)) + b[j];
+    }
+    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut), r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
+#pragma unroll
+    for (int j = 2; j < 8; ++j) {
+        r0 = mstar<T, ALGO>(r0, t0[j], lut);
+        r1 = mstar<T, ALGO>(r1, t1[j], lut);
+    }
+    return r1 - r0;
 }
 
 template <typename T>
-struct SwTask {
-    int dec, b, s;
-    int i0;         // absolute step of relative index 0 (s*W - g)
-    int len;        // steps of this sub-block
-    bool live;
-    int slot;
-    int soff;       // (b & 7) * 8 - (lane & ~7): lane's st_off -> alpha scratch column of codeword b
-    size_t nii;     // ((dec * B + b) * nS + s) * 16: this task's NII slots
-};
-
-// alpha chain position k (relative): store alpha[.][i0+k] (by state) if it lies in the
-// sub-block, save it as the NII alpha of sub-block s+1 at k = W, then step (k < n)
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T sw_alpha_at(const DecodeParams<T>& p, const WinArgs<T>& a, const SwTask<T>& t,
-                                         const LaneConst<T>& lc, const T* lut, T alpha, int k, int n)
+__device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
 {
-    const int i = t.i0 + k;
-    if (t.live && i >= t.i0 + a.g && i < t.i0 + a.g + t.len && i < p.L)
-        a.astore[t.dec][((size_t)(t.b >> 3) * p.L + i) * kLanes + lc.st_off[PH] + t.soff] = alpha;
-    if (t.live && k == a.W && t.s < a.nS - 1)
-        a.nii_wr[t.nii + 16 + (lc.st_off[PH] & 7)] = alpha;   // alpha slot of task s+1
-    if (k < n) alpha = sw_alpha_step<T, ALGO, PH>(alpha, sw_load(p, a, t.dec, t.b, i), lut, lc, i < 0);
-    return alpha;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (j == 0 || !slot0_only) ? x0 : (T)-kInfty;
 }
 
-// beta chain at relative index kr (phase PH): start the task's chain at its top, fold step
-// i = i0 + kr when it lies in the sub-block (alpha[.][i] from the scratch, beta[.][i+1] held:
-// the lane's two LLR terms are the alpha step's self / partner transitions into the state its
-// beta is held for), step, and save beta[.][i0+2g] as the NII beta of sub-block s-1
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T sw_beta_at(const DecodeParams<T>& p, const WinArgs<T>& a, const SwTask<T>& t,
-                                        const LaneConst<T>& lc, const T* lut, T beta, int kr, bool want_bits)
-{
-    const int top = t.len + 2 * a.g - 1;
-    if (kr > top) return beta;
-    const int i = t.i0 + kr;
-    if (kr == top) {   // beta[.][i+1] (labels of phase PH+1)
-        if (i + 1 >= p.L)
-            beta = t.slot == 0 ? (T)0 : (T)-kInfty;
-        else if (a.nii && a.it > 0)
-            beta = a.nii_rd[t.nii + 8 + (lc.st_off[(PH + 1) % 3] & 7)];
-        else
-            beta = (T)0;
-    }
-    const SwIn<T> x = sw_load(p, a, t.dec, t.b, i);
-    if (kr < a.g + t.len && i < p.L) {
-        const T al = a.astore[t.dec][((size_t)(t.b >> 3) * p.L + i) * kLanes + lc.st_off[PH] + t.soff];
-        const T gs = lc.a_sel[PH] ? x.Q : x.P, gp = lc.a_psel[PH] ? x.Q : x.P;
-        const T alp = dpp<PhaseDpp<PH>::ctrl>(al);
-        const T xs = fma(lc.a_sg[PH], gs, al) + beta, xp = fma(lc.a_pg[PH], gp, alp) + beta;
-        const bool us = lc.a_sg[PH] > (T)0;
-        const T m1 = sw_group_mstar<T, ALGO>(us ? xs : xp, lut), m0 = sw_group_mstar<T, ALGO>(us ? xp : xs, lut);
-        const T llr = m1 - m0;
-        if (t.live && t.slot == 0) {
-            const T le = (llr - x.la - (T)2 * x.ys) * a.ext_scale;
-            const int c = t.b & 7, g8 = t.b >> 3;
-            if (i < p.K) {
-                const int w = t.dec ? p.pi[i] : p.pinv[i];
-                a.le[t.dec][((size_t)g8 * p.K + w) * kCw + c] = le;
-                if (want_bits)
-                    p.bits[(size_t)t.b * (p.all_iters ? p.iters * p.K : p.K) + (size_t)(p.all_iters ? a.it : 0) * p.K +
-                           p.pi[i]] = llr < (T)0 ? 0 : 1;
-            }
-            if (p.le_dump) p.le_dump[(size_t)t.b * p.iters * 2 * p.L + (size_t)(2 * a.it + t.dec) * p.L + i] = le;
-        }
-    }
-    beta = sw_beta_step<T, ALGO, PH>(beta, x, lut, lc, i + 1 > p.L);   // beyond the end: hold the init
-    if (t.live && kr == 2 * a.g && t.s > 0)
-        a.nii_wr[t.nii - 16 + 8 + (lc.st_off[PH] & 7)] = beta;        // beta slot of task s-1
-    return beta;
-}
-
-template <typename T, int ALGO>
+template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[2 * kLutRows * kLutCols];
-    for (int e = threadIdx.x; e < kLutRows * kLutCols; e += blockDim.x) {
-        const int q = e / kLutCols;
-        const bool ok = q < kLutSize;
-        lut_s[e] = ok ? p.lut[q].thr : (T)INFINITY;
-        lut_s[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
+    if constexpr (ALGO == 0) {
+        for (int e = threadIdx.x; e < kLutRows * kLutCols; e += blockDim.x) {
+            const int q = e / kLutCols;
+            const bool ok = q < kLutSize;
+            lut_s[e] = ok ? p.lut[q].thr : (T)INFINITY;
+            lut_s[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const T* lut = lut_s + (lane % kLutCols);
-    LaneConst<T> lc;
-    lane_setup(p.lane, lane, lc);
-    const int per_dec = p.B * a.nS;
-    const int task = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (lane >> 3);
-    SwTask<T> t;
-    t.live = task < (a.dec < 0 ? 2 : 1) * per_dec;
-    const int tk = t.live ? task : 0;
-    t.dec = a.dec < 0 ? tk / per_dec : a.dec;
-    t.b = (tk % per_dec) / a.nS;
-    t.s = tk % a.nS;
-    t.i0 = t.s * a.W - a.g;
-    t.len = t.s == a.nS - 1 ? p.L - t.s * a.W : a.W;
-    t.slot = lane & 7;
-    t.soff = (t.b & 7) * 8 - (lane & ~7);
-    t.nii = (((size_t)t.dec * p.B + t.b) * a.nS + t.s) * 16;
-    const int wmax = p.L - (a.nS - 1) * a.W;   // the longest sub-block (uniform loop bounds)
+    // wave -> (decoder, sub-block, 64 codewords); everything but the codeword is wave-uniform
+    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const int cw_waves = a.Bp >> 6, per_dec = a.nS * cw_waves;
+    if (wv >= (a.dec < 0 ? 2 : 1) * per_dec) return;
+    const int dec = a.dec < 0 ? wv / per_dec : a.dec;
+    const int r = wv % per_dec;            // wave within the decoder: checkpoint block
+    const int s = r / cw_waves;
+    const int b_raw = (r % cw_waves) * 64 + lane;
+    const bool live = b_raw < p.B;
+    const int b = live ? b_raw : p.B - 1;
+    const int i0 = s * a.W - a.g;
+    const int len = s == a.nS - 1 ? p.L - s * a.W : a.W;
+    const size_t nii = (((size_t)dec * p.B + b) * a.nS + s) * 16;
+    T* ck = a.ckpt[dec] + (size_t)r * a.ncp * 8 * 64 + lane;
 
-    // ---- alpha: g warm-up steps, then the sub-block's steps stored by state in the alpha
-    // scratch ([G][L][64]); chains of shorter sub-blocks run on past their end unstored
-    T alpha;
-    if (t.i0 <= 0)
-        alpha = t.slot == 0 ? (T)0 : (T)-kInfty;   // the chain reaches (or starts at) step 0
+    // ---- alpha: from relative index 0 (absolute i0; steps before 0 are skipped) to g + len,
+    // a checkpoint at every S-th step of the sub-block, the NII alpha of sub-block s+1 at W
+    T al[8];
+    if (i0 <= 0)
+        sw_set(al, 1, (T)0);
     else if (a.nii && a.it > 0)
-        alpha = a.nii_rd[t.nii + (lc.st_off[0] & 7)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) al[j] = a.nii_rd[nii + j];
     else
-        alpha = (T)0;
-    const int n = a.g + wmax;
-    for (int k = 0; k <= n; k += 3) {
-        alpha = sw_alpha_at<T, ALGO, 0>(p, a, t, lc, lut, alpha, k, n);
-        if (k + 1 > n) break;
-        alpha = sw_alpha_at<T, ALGO, 1>(p, a, t, lc, lut, alpha, k + 1, n);
-        if (k + 2 > n) break;
-        alpha = sw_alpha_at<T, ALGO, 2>(p, a, t, lc, lut, alpha, k + 2, n);
-    }
-
-    // ---- beta: from relative index wmax + 2g - 1 down to g (tasks start at their own top)
-    const bool want_bits = t.dec == 1 && (p.all_iters || a.it == p.iters - 1);
-    T beta = (T)0;
-    for (int kr = wmax + 2 * a.g - 1; kr >= a.g; --kr) {
-        switch (kr % 3) {   // wave-uniform
-            case 0: beta = sw_beta_at<T, ALGO, 0>(p, a, t, lc, lut, beta, kr, want_bits); break;
-            case 1: beta = sw_beta_at<T, ALGO, 1>(p, a, t, lc, lut, beta, kr, want_bits); break;
-            default: beta = sw_beta_at<T, ALGO, 2>(p, a, t, lc, lut, beta, kr, want_bits); break;
+        sw_set(al, 0, (T)0);
+    const int n = a.g + len;
+    for (int k0 = max(0, -i0); k0 <= n; k0 += S) {
+        SwIn<T> x[S];
+#pragma unroll
+        for (int m = 0; m < S; ++m) x[m] = sw_load(p, a, dec, b, i0 + k0 + m);
+#pragma unroll
+        for (int m = 0; m < S; ++m) {
+            const int k = k0 + m;
+            if (k > n) break;
+            if (k >= a.g && k < n && ((k - a.g) % S) == 0)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ck[((size_t)((k - a.g) / S) * 8 + j) * 64] = al[j];
+            if (k == a.W && s < a.nS - 1 && live)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a.nii_wr[nii + 16 + j] = al[j];
+            if (k < n) sw_alpha_step<T, ALGO>(al, x[m], lut);
         }
     }
+    if (-i0 > a.W && s < a.nS - 1 && live)   // the NII position lies before step 0: the initial state
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a.nii_wr[nii + 16 + j] = j == 0 ? (T)0 : (T)-kInfty;
+
+    // ---- beta: warm-up from relative index len + 2g (absolute end + g) down to g + len
+    T be[8];
+    const int top = len + 2 * a.g;   // beta[.][i0 + top] starts the chain
+    if (i0 + top >= p.L)
+        sw_set(be, 1, (T)0);
+    else if (a.nii && a.it > 0)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) be[j] = a.nii_rd[nii + 8 + j];
+    else
+        sw_set(be, 0, (T)0);
+    auto nii_beta = [&](int kr) {   // beta[.][i0 + kr] is the NII beta of sub-block s-1 at kr = 2g
+        if (kr == 2 * a.g && s > 0 && live)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a.nii_wr[nii - 16 + 8 + j] = be[j];
+    };
+    if (2 * a.g >= p.L - i0) nii_beta(2 * a.g);   // NII position at or past L: the terminated state
+    for (int kr = min(top, p.L - i0) - 1; kr >= n; --kr) {   // beyond L the terminated state holds
+        sw_beta_step<T, ALGO>(be, sw_load(p, a, dec, b, i0 + kr), lut);
+        nii_beta(kr);
+    }
+
+    // ---- the sub-block, segment by segment from the last: inputs, alpha from the checkpoint,
+    // then beta + LLR backwards
+    const bool want_bits = dec == 1 && (p.all_iters || a.it == p.iters - 1);
+    for (int c = (len - 1) / S; c >= 0; --c) {
+        const int kb = a.g + c * S;   // relative index of the segment's first step
+        SwIn<T> x[S];
+        T as[S][8];
+#pragma unroll
+        for (int m = 0; m < S; ++m) x[m] = sw_load(p, a, dec, b, i0 + kb + m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) as[0][j] = ck[((size_t)c * 8 + j) * 64];
+#pragma unroll
+        for (int m = 1; m < S; ++m) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) as[m][j] = as[m - 1][j];
+            if (kb + m < n) sw_alpha_step<T, ALGO>(as[m], x[m - 1], lut);
+        }
+#pragma unroll
+        for (int m = S - 1; m >= 0; --m) {
+            const int kr = kb + m, i = i0 + kr;
+            if (kr >= n) continue;
+            const T llr = sw_llr<T, ALGO>(as[m], be, x[m], lut);
+            if (live) {
+                const T le = (llr - x[m].la - (T)2 * x[m].ys) * a.ext_scale;
+                if (i < p.K) {
+                    const int w = dec ? p.pi[i] : p.pinv[i];
+                    a.le[dec][((size_t)(b >> 3) * p.K + w) * kCw + (b & 7)] = le;
+                    if (want_bits)
+                        p.bits[(size_t)b * (p.all_iters ? p.iters * p.K : p.K) + (size_t)(p.all_iters ? a.it : 0) * p.K +
+                               p.pi[i]] = llr < (T)0 ? 0 : 1;
+                }
+                if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * p.L + (size_t)(2 * a.it + dec) * p.L + i] = le;
+            }
+            sw_beta_step<T, ALGO>(be, x[m], lut);
+            nii_beta(kr);
+        }
+    }
+}
+
+template <typename T>
+constexpr int sw_seg()
+{
+    return sizeof(T) == 4 ? 8 : 4;   // checkpoint spacing S: the segment's alpha stays in registers
 }
 
 template <typename T, int ALGO>
 hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)
 {
+    constexpr int S = sw_seg<T>();
     const int W = w.window;
-    const int nS = p.L / W > 0 ? p.L / W : 1;
+    const int nS = window_subblocks(p.L, W);
     WinArgs<T> a{};
     a.W = W;
     a.g = w.overlap;
     a.nS = nS;
+    a.Bp = (p.B + 63) / 64 * 64;
+    a.ncp = (p.L - (nS - 1) * W + S - 1) / S;
     a.ext_scale = (T)w.ext_scale;
     a.nii = w.nii;
-    a.astore[0] = wb.astore[0];
-    a.astore[1] = wb.astore[1];
+    a.ckpt[0] = wb.ckpt[0];
+    a.ckpt[1] = wb.ckpt[1];
     const size_t nii_half = (size_t)2 * p.B * nS * 16;
     for (int it = 0; it < p.iters; ++it) {
         a.it = it;
@@ -1170,14 +1206,22 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 a.la[0] = a.le[1] = wb.ext21[0];
                 a.la[1] = a.le[0] = wb.ext12[0];
             }
-            const long long tasks = (long long)p.B * nS * (w.concurrent ? 2 : 1);
-            const int blocks = (int)((tasks + 31) / 32);   // 4 waves x 8 tasks per block
-            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO>), dim3(blocks), dim3(256), 0, st, p, a);
+            const long long waves = (long long)nS * (a.Bp / 64) * (w.concurrent ? 2 : 1);
+            const int blocks = (int)((waves + 3) / 4);
+            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
     }
     return hipSuccess;
+}
+
+size_t window_ckpt_elems(int B, int L, int W, bool f32)
+{
+    const int S = f32 ? sw_seg<float>() : sw_seg<double>();
+    const int nS = window_subblocks(L, W);
+    const size_t ncp = (size_t)(L - (nS - 1) * W + S - 1) / S;
+    return (size_t)nS * ((B + 63) / 64) * ncp * 8 * 64;
 }
 
 template <typename T>

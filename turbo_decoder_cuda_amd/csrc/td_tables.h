@@ -41,6 +41,8 @@ struct Trellis {
 // metric +-Q" (p in {2,3,4,5}; +-P otherwise).  td_create checks build_trellis(13, 15) against them.
 constexpr int kTrellisLast[kStates][2] = {{0, 1}, {3, 2}, {4, 5}, {7, 6}, {1, 0}, {2, 3}, {5, 4}, {6, 7}};
 constexpr int kTrellisQ[kStates] = {0, 0, 1, 1, 1, 1, 0, 0};
+// nextstat[s][u] (log_map.h:58-66) of the same trellis
+constexpr int kTrellisNext[kStates][2] = {{0, 4}, {4, 0}, {5, 1}, {1, 5}, {2, 6}, {6, 2}, {7, 3}, {3, 7}};
 
 // gen_g_matrix (log_map.cpp:114-169): octal -> 4 binary taps, MSB first. false on a non-octal digit.
 inline bool octal_taps(int g, int* taps)
@@ -102,6 +104,7 @@ inline bool trellis_is_lte(const Trellis& t)
             // u == 1 with parity +1, or u == 0 with parity -1: +-P; otherwise +-Q (see td_kernels.hip "gamma")
             const int o = t.nextout[p][2 * u + 1];
             if ((((u == 1) == (o == 1)) ? 0 : 1) != kTrellisQ[p]) return false;
+            if (t.nextstat[j][u] != kTrellisNext[j][u]) return false;
         }
     return true;
 }
