@@ -986,7 +986,17 @@ __device__ __forceinline__ T sw_g(const SwIn<T>& x, int s)
     return kTrellisQ[s] ? x.Q : x.P;
 }
 
-// alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-1001), max-normalised
+// metrics -= their max (log_map.cpp:995-1000).  The windowed chains normalise only every S
+// steps: max* is shift-invariant, and S steps of growth stay far inside the type's range
+template <typename T>
+__device__ __forceinline__ void sw_normalise(T (&v)[8])
+{
+    const T m = vmax(vmax(vmax(v[0], v[1]), vmax(v[2], v[3])), vmax(vmax(v[4], v[5]), vmax(v[6], v[7])));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] - m;
+}
+
+// alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-1001)
 template <typename T, int ALGO>
 __device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const T* lut)
 {
@@ -996,12 +1006,11 @@ __device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const
         const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
         n[j] = mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
     }
-    const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = n[j] - m;
+    for (int j = 0; j < 8; ++j) a[j] = n[j];
 }
 
-// beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1021), max-normalised
+// beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1021)
 template <typename T, int ALGO>
 __device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const T* lut)
 {
@@ -1011,9 +1020,8 @@ __device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const 
         const T G = sw_g(x, j);
         n[j] = mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
     }
-    const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = n[j] - m;
+    for (int j = 0; j < 8; ++j) b[j] = n[j];
 }
 
 // LLR of step i (log_map.cpp:1024-1039): the two left folds of E over the 8 next states
@@ -1092,9 +1100,13 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
         for (int m = 0; m < S; ++m) {
             const int k = k0 + m;
             if (k > n) break;
-            if (k >= a.g && k < n && ((k - a.g) % S) == 0)
+            if (k >= a.g && k < n && ((k - a.g) % S) == 0) {
+                sw_normalise(al);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) ck[((size_t)((k - a.g) / S) * 8 + j) * 64] = al[j];
+            } else if (k < a.g && m == 0) {
+                sw_normalise(al);   // warm-up
+            }
             if (k == a.W && s < a.nS - 1 && live)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) a.nii_wr[nii + 16 + j] = al[j];
@@ -1123,6 +1135,7 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
     if (2 * a.g >= p.L - i0) nii_beta(2 * a.g);   // NII position at or past L: the terminated state
     for (int kr = min(top, p.L - i0) - 1; kr >= n; --kr) {   // beyond L the terminated state holds
         sw_beta_step<T, ALGO>(be, sw_load(p, a, dec, b, i0 + kr), lut);
+        if (kr % S == 0) sw_normalise(be);
         nii_beta(kr);
     }
 
@@ -1160,6 +1173,7 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
                 if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * p.L + (size_t)(2 * a.it + dec) * p.L + i] = le;
             }
             sw_beta_step<T, ALGO>(be, x[m], lut);
+            if (m == 0) sw_normalise(be);
             nii_beta(kr);
         }
     }
