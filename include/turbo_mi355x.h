@@ -143,6 +143,20 @@ int td_synth_seek(td_handle* h, unsigned long long frame);
 int td_rand_window(unsigned seed, unsigned long long draws, uint32_t* win);
 int td_synth_frames(td_handle* h, double ebn0_db, int B, uint8_t* d_info, double* d_llr, void* stream);
 
+/* Modulation of the generator's frames (MODULATION, main.cpp:13-15, 174, 197-202): 1 = BPSK
+ * (default), 2 = QPSK, 3 = 8PSK, 4 = 16QAM, 6 = 64QAM bits per symbol; SYMBOL_NUM = (3K+12)/M
+ * symbols, sigma = 10^(-EbN0/20) sqrt(0.5 / (rate M)) with rate = K / SYMBOL_NUM.  TD_EINVAL when
+ * 3K+12 is not a multiple of M. */
+int td_synth_modulation(td_handle* h, int modulation);
+
+/* Replaces module (modanddem.cpp:175-187, _bpsk/_qpsk/_8psk/_16qam/_64qam_module :88-173) on
+ * device arrays: d_bits [nsym * modulation] uint8 (0/1; the reference takes int) -> d_si, d_sq [nsym]. */
+int td_modulate(const uint8_t* d_bits, long long nsym, int modulation, double* d_si, double* d_sq, void* stream);
+/* Replaces demodule (modanddem.cpp:674-685, the max-log demappers :189-671) on device arrays:
+ * d_yi, d_yq [nsym] received symbols -> d_llr [nsym * modulation], bit-exact with the reference. */
+int td_demodulate(const double* d_yi, const double* d_yq, long long nsym, int modulation, double Kf, double* d_llr,
+                  void* stream);
+
 /* Error counts per frame and iteration for the BER harness (main.cpp:224-237):
  * d_err[b][it] = #{i < K : d_bits[b][it][i] != d_info[b][i]}, d_bits as td_decode_device's
  * all_iters output with `iters` rows. */

@@ -71,6 +71,10 @@ def lib():
         L.tdo_glibc_rand_next.restype = C.c_int
         L.tdo_make_frame.argtypes = [C.POINTER(Trellis), P, C.c_int, C.c_double, C.POINTER(GlibcRand), P, P]
         L.tdo_mgrns.argtypes = [C.c_double, C.c_double, C.c_double, C.c_int, P]
+        L.tdo_modulate.argtypes = [P, C.c_int, C.c_int, P, P]
+        L.tdo_demodulate.argtypes = [P, P, C.c_int, C.c_int, C.c_double, P]
+        L.tdo_make_frame_mod.argtypes = [C.POINTER(Trellis), P, C.c_int, C.c_double, C.c_int, C.POINTER(GlibcRand),
+                                         P, P]
         _lib = L
     return _lib
 
@@ -163,6 +167,37 @@ def make_frames(K: int, f1: int, f2: int, ebn0_db: float, seed: int, nframes: in
     flows = np.zeros((nframes, 3 * K + 12), dtype=np.float64)
     for i in range(nframes):
         lib().tdo_make_frame(C.byref(t), _p(pi), K, ebn0_db, C.byref(g), _p(srcs[i]), _p(flows[i]))
+    return srcs, flows
+
+
+def modulate(bits: np.ndarray, M: int):
+    """module() (modanddem.cpp:175): bits -> (symbols_i, symbols_q)."""
+    bits = np.ascontiguousarray(bits, dtype=np.int32)
+    n = bits.size // M
+    si, sq = np.zeros(n), np.zeros(n)
+    assert lib().tdo_modulate(_p(bits), bits.size, M, _p(si), _p(sq)) == 0
+    return si, sq
+
+
+def demodulate(yi: np.ndarray, yq: np.ndarray, M: int, Kf: float) -> np.ndarray:
+    """demodule() (modanddem.cpp:674): max-log bit LLRs [M * nsym]."""
+    yi = np.ascontiguousarray(yi, dtype=np.float64)
+    yq = np.ascontiguousarray(yq, dtype=np.float64)
+    out = np.zeros(yi.size * M)
+    assert lib().tdo_demodulate(_p(yi), _p(yq), yi.size, M, Kf, _p(out)) == 0
+    return out
+
+
+def make_frames_mod(K: int, f1: int, f2: int, ebn0_db: float, M: int, seed: int, nframes: int):
+    """main.cpp's frames with MODULATION = M (SYMBOL_NUM = (3K+12)/M), srand(seed)."""
+    g = GlibcRand()
+    lib().tdo_glibc_srand(C.byref(g), seed)
+    t = trellis()
+    pi = qpp(K, f1, f2)
+    srcs = np.zeros((nframes, K), dtype=np.int32)
+    flows = np.zeros((nframes, 3 * K + 12), dtype=np.float64)
+    for i in range(nframes):
+        lib().tdo_make_frame_mod(C.byref(t), _p(pi), K, ebn0_db, M, C.byref(g), _p(srcs[i]), _p(flows[i]))
     return srcs, flows
 
 

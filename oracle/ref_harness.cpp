@@ -10,6 +10,8 @@
 //   maxstar n seed out                            -- E_algorithm on random + edge pairs (:779)
 //   ber K f1 f2 iters ebn0 maxframes minerr seed  -- BER/BLER via TurboDecoding (prints one line)
 //   time K f1 f2 nframes                          -- ms per TurboDecoding call (15 iterations)
+//   demod M nsym seed out                         -- demodule() on random + constellation-point symbols
+//   framesmod K f1 f2 M ebn0 seed nframes out     -- main.cpp frames with MODULATION = M (src, flow)
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -44,12 +46,12 @@ extern int M_num_reg;
 
 static const int kRefIters = 15;   // N_ITERATION, log_map.h:30
 
-static void setup(int K, int a, int b)
+static void setup(int K, int a, int b, int M = 1)
 {
-    MODULATION = 1;
+    MODULATION = M;   // the argv configuration of main.cpp:13-15
     source_length = K;
     length_after_code = 3 * K + 12;
-    SYMBOL_NUM = length_after_code;
+    SYMBOL_NUM = length_after_code / M;
     f1 = a;
     f2 = b;
     TurboCodingInit();
@@ -249,6 +251,68 @@ static int mode_time(int argc, char** argv)
     return 0;
 }
 
+// demodule() (modanddem.cpp:674) on nsym symbols: uniform in [-2, 2]^2, plus every
+// constellation point of every modulation exactly, plus points midway between levels
+static int mode_demod(int argc, char** argv)
+{
+    if (argc != 6) return 2;
+    int M = atoi(argv[2]), nsym = atoi(argv[3]);
+    srand((unsigned)strtoul(argv[4], 0, 10));
+    std::vector<int> bits(64 * 6);
+    std::vector<double> yi(nsym), yq(nsym), ci(64), cq(64), out((size_t)nsym * M);
+    int k = 0;
+    const int Ms[5] = {1, 2, 3, 4, 6};
+    for (int mi = 0; mi < 5; mi++) {   // the constellation points, through module()
+        const int m = Ms[mi];
+        for (int j = 0; j < (1 << m); j++)
+            for (int b = 0; b < m; b++) bits[(size_t)j * m + b] = (j >> (m - 1 - b)) & 1;
+        module(bits.data(), ci.data(), cq.data(), (1 << m) * m, m);
+        for (int j = 0; j < (1 << m) && k < nsym; j++, k++) {
+            yi[k] = ci[j];
+            yq[k] = cq[j];
+        }
+    }
+    for (int j = 0; j < 8 && k < nsym; j++, k++) {   // on the 16QAM / 64QAM decision boundaries
+        yi[k] = (j & 1 ? 0.632456 : 0.0) * (j & 2 ? -1 : 1);
+        yq[k] = (j & 4 ? 0.3086 : 0.0);
+    }
+    for (; k < nsym; k++) {
+        yi[k] = 4.0 * rand() / RAND_MAX - 2.0;
+        yq[k] = 4.0 * rand() / RAND_MAX - 2.0;
+    }
+    demodule(yi.data(), yq.data(), nsym, out.data(), 1.7, M);
+    FILE* f = must_open(argv[5]);
+    fwrite(yi.data(), sizeof(double), nsym, f);
+    fwrite(yq.data(), sizeof(double), nsym, f);
+    fwrite(out.data(), sizeof(double), out.size(), f);
+    fclose(f);
+    return 0;
+}
+
+// main.cpp:170-202 frames with MODULATION = M: src [K] int32 + flow [3K+12] double per frame
+static int mode_framesmod(int argc, char** argv)
+{
+    if (argc != 10) return 2;
+    int K = atoi(argv[2]), a = atoi(argv[3]), b = atoi(argv[4]), M = atoi(argv[5]);
+    double ebn0 = atof(argv[6]);
+    unsigned seed = (unsigned)strtoul(argv[7], 0, 10);
+    int nf = atoi(argv[8]);
+    setup(K, a, b, M);
+    const int n = 3 * K + 12;
+    FILE* f = must_open(argv[9]);
+    srand(seed);
+    std::vector<int> src(K);
+    std::vector<double> flow(n);
+    for (int fr = 0; fr < nf; fr++) {
+        make_frame(K, ebn0, src.data(), flow.data());
+        fwrite(src.data(), sizeof(int), K, f);
+        fwrite(flow.data(), sizeof(double), n, f);
+    }
+    fclose(f);
+    TurboCodingRelease();
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 2) return 2;
@@ -257,6 +321,8 @@ int main(int argc, char** argv)
     if (!strcmp(argv[1], "maxstar")) return mode_maxstar(argc, argv);
     if (!strcmp(argv[1], "ber")) return mode_ber(argc, argv);
     if (!strcmp(argv[1], "time")) return mode_time(argc, argv);
+    if (!strcmp(argv[1], "demod")) return mode_demod(argc, argv);
+    if (!strcmp(argv[1], "framesmod")) return mode_framesmod(argc, argv);
     fprintf(stderr, "unknown mode\n");
     return 2;
 }

@@ -225,6 +225,74 @@ void tdo_bpsk_demod(const double* yi, const double* yq, int n, double Kf, double
     }
 }
 
+/* Constellations of modanddem.cpp:7-71, indexed by the symbol's label (module's bit order). */
+static const double k_qpsk_i[4] = {0.7071, 0.7071, -0.7071, -0.7071};
+static const double k_qpsk_q[4] = {0.7071, -0.7071, 0.7071, -0.7071};
+static const double k_8psk_i[8] = {-0.7071, -1, 0, 0.7071, 0, -0.7071, 0.7071, 1};
+static const double k_8psk_q[8] = {0.7071, 0, 1, 0.7071, -1, -0.7071, -0.7071, 0};
+static const double k_16qam_a = 0.948683, k_16qam_b = 0.316228;
+static const double k_64qam[4] = {0.4629, 0.1543, 0.7615, 1.0801};
+
+/* constellation point of label j for M bits per symbol */
+static void constellation(int M, int j, double* ci, double* cq)
+{
+    switch (M) {
+    case 1: *ci = j ? 1.0 : -1.0; *cq = 0.0; break;
+    case 2: *ci = k_qpsk_i[j]; *cq = k_qpsk_q[j]; break;
+    case 3: *ci = k_8psk_i[j]; *cq = k_8psk_q[j]; break;
+    case 4: {   /* i from the two high label bits {-a,-b,a,b}, q from the two low bits {-a,-b,a,b} */
+        const double lv[4] = {-k_16qam_a, -k_16qam_b, k_16qam_a, k_16qam_b};
+        *ci = lv[j >> 2];
+        *cq = lv[j & 3];
+        break;
+    }
+    default: {  /* 64QAM: sign from bit 5 (i) / bit 2 (q), level from bits 4-3 (i) / 1-0 (q) */
+        *ci = ((j >> 5) & 1 ? -1.0 : 1.0) * k_64qam[(j >> 3) & 3];
+        *cq = ((j >> 2) & 1 ? -1.0 : 1.0) * k_64qam[j & 3];
+        break;
+    }
+    }
+}
+
+int tdo_modulate(const int* bits, int N, int M, double* oi, double* oq)
+{
+    if (M != 1 && M != 2 && M != 3 && M != 4 && M != 6) return -1;
+    for (int s = 0; s < N / M; s++) {
+        int j = 0;
+        if (M == 3)   /* _8psk_module: the symbol's first bit is the label's LSB (:135) */
+            for (int b = 0; b < 3; b++) j |= bits[3 * s + b] << b;
+        else          /* the others: first bit is the MSB (:113,:150,:165) */
+            for (int b = 0; b < M; b++) j = j * 2 + bits[M * s + b];
+        constellation(M, j, &oi[s], &oq[s]);
+    }
+    return 0;
+}
+
+int tdo_demodulate(const double* yi, const double* yq, int nsym, int M, double Kf, double* out)
+{
+    if (M != 1 && M != 2 && M != 3 && M != 4 && M != 6) return -1;
+    const double big = 0x7fffffffffff, small = 0x7fffffff;   /* the functions' initial minima */
+    for (int i = 0; i < nsym; i++)
+        for (int b = 0; b < M; b++) {
+            /* output bit b of the symbol is label bit (M-1-b), except 8PSK's (label bit b) */
+            const int mask = M == 3 ? 1 << b : 1 << (M - 1 - b);
+            double m1 = (M <= 2) ? big : small;
+            double m2 = (M == 1 || (M == 2 && b == 0)) ? big : small;
+            for (int j = 0; j < (1 << M); j++) {
+                double ci, cq;
+                constellation(M, j, &ci, &cq);
+                const double d = sqr_dis(yi[i], yq[i], ci, cq);
+                if (j & mask) {
+                    if (d < m1) m1 = d;
+                } else {
+                    if (d < m2) m2 = d;
+                }
+            }
+            out[(size_t)M * i + b] = -Kf * (m1 - m2);
+        }
+    return 0;
+}
+
 /* glibc srandom_r/random_r, TYPE_3 (degree 31, separation 3) */
 void tdo_glibc_srand(tdo_glibc_rand* g, unsigned seed)
 {
@@ -274,6 +342,28 @@ void tdo_make_frame(const tdo_trellis* t, const int* pi, int K, double ebn0_db, 
     tdo_awgn(si, ri, sigma, n, awgn_seed(g));
     tdo_awgn(sq, rq, sigma, n, awgn_seed(g));
     tdo_bpsk_demod(ri, rq, n, 1 / (2 * pow(sigma, 2)), flow);
+    free(coded);
+    free(si);
+    free(sq);
+    free(ri);
+    free(rq);
+}
+
+void tdo_make_frame_mod(const tdo_trellis* t, const int* pi, int K, double ebn0_db, int M, tdo_glibc_rand* g,
+                        int* src, double* flow)
+{
+    const int n = 3 * K + 4 * TDO_MREG, nsym = n / M;
+    const double rate = (double)K / (double)nsym;
+    const double sigma = pow(10, -ebn0_db / 20) * sqrt(0.5 / (rate * M));
+    int* coded = (int*)malloc(sizeof(int) * n);
+    double *si = (double*)malloc(sizeof(double) * nsym), *sq = (double*)malloc(sizeof(double) * nsym);
+    double *ri = (double*)malloc(sizeof(double) * nsym), *rq = (double*)malloc(sizeof(double) * nsym);
+    for (int i = 0; i < K; i++) src[i] = tdo_glibc_rand_next(g) % 2;
+    tdo_turbo_encode(t, pi, src, K, coded);
+    tdo_modulate(coded, nsym * M, M, si, sq);
+    tdo_awgn(si, ri, sigma, nsym, awgn_seed(g));
+    tdo_awgn(sq, rq, sigma, nsym, awgn_seed(g));
+    tdo_demodulate(ri, rq, nsym, M, 1 / (2 * pow(sigma, 2)), flow);
     free(coded);
     free(si);
     free(sq);

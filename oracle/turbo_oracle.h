@@ -67,6 +67,17 @@ int tdo_glibc_rand_next(tdo_glibc_rand* g);
 void tdo_make_frame(const tdo_trellis* t, const int* pi, int K, double ebn0_db, tdo_glibc_rand* g,
                     int* src, double* flow);
 
+/* modanddem.cpp:175-187 (module) for M = 1, 2, 3, 4, 6 bits per symbol: N bits -> N/M symbols
+ * (_bpsk/_qpsk/_8psk/_16qam/_64qam_module, :88-173; constellations :7-71).  Returns 0, -1 on a bad M. */
+int tdo_modulate(const int* bits, int N, int M, double* out_i, double* out_q);
+/* modanddem.cpp:674-685 (demodule): max-log bit LLRs of nsym symbols, out[M*nsym]
+ * (_bpsk/_qpsk/_8psk/_16qam/_64qam_demodule, :189-671).  Returns 0, -1 on a bad M. */
+int tdo_demodulate(const double* yi, const double* yq, int nsym, int M, double Kf, double* out);
+/* One frame of main.cpp:183-202 with MODULATION = M and SYMBOL_NUM = (3K+12)/M (the argv
+ * configuration, main.cpp:13-15): rate = K/SYMBOL_NUM, sigma = 10^(-EbN0/20) sqrt(0.5/(rate M)). */
+void tdo_make_frame_mod(const tdo_trellis* t, const int* pi, int K, double ebn0_db, int M, tdo_glibc_rand* g,
+                        int* src, double* flow);
+
 /* Jacobian max* with the 16-step table, log_map.cpp:14-18,779-801 */
 double tdo_maxstar(double x, double y);
 /* left fold, log_map.cpp:817-829 */

@@ -4,6 +4,8 @@ The product is libturbo_mi355x.so (C ABI: include/turbo_mi355x.h, HIP kernels fo
 csrc/).  This package holds its build script and a thin host-side mirror of the reference
 codec interface (decoder.py).  See DESIGN.md.
 """
-from .decoder import N_ITERATION, TERMINATED, TurboCodec, TurboCodingInit, device_count, stream_length
+from .decoder import (N_ITERATION, TERMINATED, TurboCodec, TurboCodingInit, demodulate, device_count, modulate,
+                      stream_length)
 
-__all__ = ["TurboCodec", "TurboCodingInit", "N_ITERATION", "TERMINATED", "device_count", "stream_length"]
+__all__ = ["TurboCodec", "TurboCodingInit", "N_ITERATION", "TERMINATED", "device_count", "stream_length",
+           "modulate", "demodulate"]

@@ -21,7 +21,7 @@ EXPORTS = (
     "td_last_error", "td_device_count", "td_abi_version", "td_maxstar_host_f64", "td_maxstar_host_f32",
     "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read", "td_debug_set_stamps",
     "td_debug_stamp_slots", "td_synth_seed", "td_synth_frames", "td_count_errors", "td_rand_window", "td_synth_seek",
-    "td_set_window",
+    "td_set_window", "td_synth_modulation", "td_modulate", "td_demodulate",
 )
 
 
@@ -85,6 +85,9 @@ def lib() -> C.CDLL:
     L.td_synth_frames.argtypes = [P, C.c_double, I, P, P, P]
     L.td_count_errors.argtypes = [P, P, I, P, I, P, P]
     L.td_set_window.argtypes = [P, C.POINTER(TdWindowParams)]
+    L.td_synth_modulation.argtypes = [P, I]
+    L.td_modulate.argtypes = [P, C.c_longlong, I, P, P, P]
+    L.td_demodulate.argtypes = [P, P, C.c_longlong, I, C.c_double, P, P]
     _lib = L
     return L
 

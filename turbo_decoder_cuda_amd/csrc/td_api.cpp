@@ -66,6 +66,7 @@ struct td_handle {
     unsigned long long lfg_frames = 0;
     uint32_t* d_win = nullptr;
     int win_cap = 0;
+    int modulation = 1;                          // td_synth_modulation (MODULATION)
     // decoding schedule (td_set_window): window 0 = exact full trellis
     td::WindowParams wp{0, 0, 0, 0, 1.0f};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
@@ -708,13 +709,47 @@ int td_synth_frames(td_handle* h, double ebn0_db, int B, uint8_t* d_info, double
     }
     h->lfg_frames += (unsigned long long)B;
     TD_HIP(hipMemcpyAsync(h->d_win, wins.data(), wins.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    const int K = h->p.K, n = 3 * K + 4 * td::kMemory;
-    const double rate = (double)K / (double)n;                                      // main.cpp:47
-    const double sigma = std::pow(10.0, -ebn0_db / 20) * std::sqrt(0.5 / (rate * 1));   // main.cpp:174
-    td::SynthParams sp{K, n, B, h->d_pi, h->d_win, sigma, 1 / (2 * std::pow(sigma, 2)), d_info, d_llr};
+    const int K = h->p.K, n = 3 * K + 4 * td::kMemory, M = h->modulation;
+    const int nsym = n / M;                                                         // SYMBOL_NUM, main.cpp:15
+    const double rate = (double)K / (double)nsym;                                   // main.cpp:47
+    const double sigma = std::pow(10.0, -ebn0_db / 20) * std::sqrt(0.5 / (rate * M));   // main.cpp:174
+    td::SynthParams sp{K, n, B, M, h->d_pi, h->d_win, sigma, 1 / (2 * std::pow(sigma, 2)), d_info, d_llr};
     TD_HIP(td::launch_synth(sp, st));
     // the host window buffer must outlive the async copy
     TD_HIP(hipStreamSynchronize(st));
+    return TD_OK;
+}
+
+int td_synth_modulation(td_handle* h, int modulation)
+{
+    if (!h) return fail(TD_EINVAL, "td_synth_modulation: null handle");
+    const int n = 3 * h->p.K + 4 * td::kMemory;
+    if (modulation != 1 && modulation != 2 && modulation != 3 && modulation != 4 && modulation != 6)
+        return fail(TD_EINVAL, "td_synth_modulation: modulation must be 1, 2, 3, 4 or 6 bits per symbol");
+    if (n % modulation)
+        return fail(TD_EINVAL, "td_synth_modulation: 3K+12 = " + std::to_string(n) + " is not a whole number of symbols");
+    h->modulation = modulation;
+    return TD_OK;
+}
+
+int td_modulate(const uint8_t* d_bits, long long nsym, int modulation, double* d_si, double* d_sq, void* stream)
+{
+    if (!d_bits || !d_si || !d_sq || nsym < 0) return fail(TD_EINVAL, "td_modulate: bad argument");
+    if (nsym == 0) return TD_OK;
+    const hipError_t e = td::launch_modulate(d_bits, nsym, modulation, d_si, d_sq, static_cast<hipStream_t>(stream));
+    if (e == hipErrorInvalidValue) return fail(TD_EINVAL, "td_modulate: modulation must be 1, 2, 3, 4 or 6");
+    TD_HIP(e);
+    return TD_OK;
+}
+
+int td_demodulate(const double* d_yi, const double* d_yq, long long nsym, int modulation, double Kf, double* d_llr,
+                  void* stream)
+{
+    if (!d_yi || !d_yq || !d_llr || nsym < 0) return fail(TD_EINVAL, "td_demodulate: bad argument");
+    if (nsym == 0) return TD_OK;
+    const hipError_t e = td::launch_demodulate(d_yi, d_yq, nsym, modulation, Kf, d_llr, static_cast<hipStream_t>(stream));
+    if (e == hipErrorInvalidValue) return fail(TD_EINVAL, "td_demodulate: modulation must be 1, 2, 3, 4 or 6");
+    TD_HIP(e);
     return TD_OK;
 }
 

@@ -89,6 +89,7 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 // device frame generator (td_synth.hip): main.cpp's frame, one thread per frame
 struct SynthParams {
     int K, n, B;
+    int M;                  // bits per symbol (MODULATION): 1, 2, 3, 4, 6
     const int* pi;          // [K] QPP
     const uint32_t* win;    // [B][31] glibc random_r window at each frame's first draw
     double sigma, Kf;       // main.cpp:174 sigma; demodule's 1/(2 sigma^2), computed on the host
@@ -96,6 +97,10 @@ struct SynthParams {
     double* flow;           // [B][3K+12] channel LLRs out (fp64, the reference's type)
 };
 hipError_t launch_synth(const SynthParams& p, hipStream_t st);
+// module / demodule (modanddem.cpp:175, :674) on device arrays
+hipError_t launch_modulate(const uint8_t* bits, long long nsym, int M, double* si, double* sq, hipStream_t st);
+hipError_t launch_demodulate(const double* yi, const double* yq, long long nsym, int M, double Kf, double* out,
+                             hipStream_t st);
 hipError_t launch_count_errors(const uint8_t* bits, const uint8_t* info, int K, int iters, int B, int* err,
                                hipStream_t st);
 

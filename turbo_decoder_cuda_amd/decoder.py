@@ -136,6 +136,10 @@ class TurboCodec:
         """srand(seed) for the handle's frame stream (main.cpp:170)."""
         N.check(N.lib().td_synth_seed(self._h, int(seed) & 0xFFFFFFFF))
 
+    def synth_modulation(self, modulation: int) -> None:
+        """MODULATION of the generator's frames: 1 BPSK, 2 QPSK, 3 8PSK, 4 16QAM, 6 64QAM."""
+        N.check(N.lib().td_synth_modulation(self._h, int(modulation)))
+
     def synth_seek(self, frame: int) -> None:
         N.check(N.lib().td_synth_seek(self._h, int(frame)))
 
@@ -181,6 +185,34 @@ class TurboCodec:
         N.check(N.lib().td_siso_host(self._h, recs2.ctypes.data_as(C.c_void_p), La2.ctypes.data_as(C.c_void_p),
                                      int(terminated), out.ctypes.data_as(C.c_void_p), L, B))
         return out[0] if one else out
+
+
+def modulate(bits, modulation: int, stream=None):
+    """module (modanddem.cpp:175) on the GPU: uint8 bits [nsym * M] (cuda) -> (si, sq) float64."""
+    import torch
+
+    bits = bits.contiguous()
+    nsym = bits.numel() // modulation
+    si = torch.empty(nsym, dtype=torch.float64, device=bits.device)
+    sq = torch.empty_like(si)
+    if stream is None:
+        stream = torch.cuda.current_stream(bits.device)
+    N.check(N.lib().td_modulate(C.c_void_p(bits.data_ptr()), nsym, int(modulation), C.c_void_p(si.data_ptr()),
+                                C.c_void_p(sq.data_ptr()), C.c_void_p(stream.cuda_stream)))
+    return si, sq
+
+
+def demodulate(yi, yq, modulation: int, Kf: float, stream=None):
+    """demodule (modanddem.cpp:674) on the GPU: float64 symbols [nsym] (cuda) -> LLRs [nsym * M]."""
+    import torch
+
+    yi, yq = yi.contiguous(), yq.contiguous()
+    out = torch.empty(yi.numel() * modulation, dtype=torch.float64, device=yi.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(yi.device)
+    N.check(N.lib().td_demodulate(C.c_void_p(yi.data_ptr()), C.c_void_p(yq.data_ptr()), yi.numel(), int(modulation),
+                                  float(Kf), C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)))
+    return out
 
 
 def TurboCodingInit(K: int, f1: int, f2: int, **kw) -> TurboCodec:
