@@ -133,6 +133,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(a, llr_h, bits.cpu().numpy(), f1, f2)
     if rank == 0 and world == 1 and not a.no_variants:
         out["variants"] = variants(a, llr64, u_d, f1, f2, dev, stream)
+        out["demod"] = demod_rates(a, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -287,6 +288,34 @@ def variants(a, llr64, u_d, f1, f2, dev, stream):
         res[f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else "")] = {"value": round(a.batch * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s",
                                  "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4),
                                  "bit_errors": errs}
+    return res
+
+
+def demod_rates(a, dev):
+    """td_demodulate (modanddem.cpp:674) over one batch's symbols per
+    modulation: HBM roofline with 16 B in + 8 M B out per symbol."""
+    import torch
+
+    from turbo_decoder_cuda_amd import demodulate
+    res = {}
+    g = torch.Generator(device=dev).manual_seed(5)
+    for M in (1, 2, 4, 6):
+        nsym = a.batch * (3 * a.K + 12) // M
+        yi = torch.randn(nsym, dtype=torch.float64, device=dev, generator=g)
+        yq = torch.randn(nsym, dtype=torch.float64, device=dev, generator=g)
+        out = demodulate(yi, yq, M, 1.3)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        e0.record()
+        for _ in range(reps):
+            demodulate(yi, yq, M, 1.3)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        gbs = nsym * (16 + 8 * M) / (ms * 1e-3) / 1e9
+        res[f"M{M}"] = {"symbols": nsym, "ms": round(ms, 4), "Msym_per_s": round(nsym / ms / 1e3, 1),
+                        "GB_per_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        del yi, yq, out
     return res
 
 

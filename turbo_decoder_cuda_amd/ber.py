@@ -98,7 +98,7 @@ def write_result_txt(path: str, points, K: int, ebn0_start: float, ebn0_step: fl
                      modulation: int = 1):
     """Append a block in main.cpp's result.txt format (main.cpp:80-99, 264-315)."""
     n = stream_length(K)
-    rate = K / n
+    rate = K / (n // modulation)   # main.cpp:47: source_length / SYMBOL_NUM
     with open(path, "a") as fp:
         fp.write(f"\nMODULATION = {modulation}")
         fp.write(f"\nsource_length = {K}")
@@ -142,6 +142,8 @@ def main(argv=None):
     ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--modulation", type=int, default=1, choices=[1, 2, 3, 4, 6],
+                    help="MODULATION of the frames (bits per symbol, modanddem.cpp)")
     ap.add_argument("--window", type=int, default=0, help="sub-block length (0 = exact schedule)")
     ap.add_argument("--overlap", type=int, default=0)
     ap.add_argument("--nii", action="store_true")
@@ -161,6 +163,7 @@ def main(argv=None):
         a.algo, a.precision = "maxlog", "f32"
         a.window, a.overlap, a.nii, a.concurrent, a.ext_scale = a.K // a.reference_gpu, 0, True, True, 0.77
     with TurboCodec(a.K, a.f1, a.f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=a.device) as c:
+        c.synth_modulation(a.modulation)
         if a.window:
             c.set_window(a.window, a.overlap, a.ext_scale, nii=a.nii, concurrent=a.concurrent)
         res = ber_sweep(c, pts, a.seed, a.max_frames, a.min_block_errors, a.batch,
@@ -169,7 +172,7 @@ def main(argv=None):
         print(f"{p.ebn0_db:.2f} frames {p.frames} " +
               " ".join(f"{be}:{bl}" for be, bl in zip(p.bit_errors, p.block_errors)))
     if a.out:
-        write_result_txt(a.out, res, a.K, start, step, end)
+        write_result_txt(a.out, res, a.K, start, step, end, modulation=a.modulation)
     return 0
 
 
