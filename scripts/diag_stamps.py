@@ -48,3 +48,26 @@ distinct = np.array([len(set(simd[g])) for g in range(G)])
 print("  waves of a group on distinct SIMDs: " + ", ".join(f"{k}:{int((distinct == k).sum())}" for k in (1, 2, 3, 4)))
 same = lambda a, b: int((simd[:, a] == simd[:, b]).sum())
 print(f"  A/B share SIMD in {same(0, 1)} groups, A/F0 {same(0, 2)}, A/F1 {same(0, 3)}, B/F0 {same(1, 2)}, B/F1 {same(1, 3)}")
+# workgroups resident on the same CU (XCC, SE, SH, CU): which roles of the two share a SIMD
+xcc = st.cpu().numpy().reshape(G, 4, 7)[:, 0, 5].astype(np.int64) & 0xF
+sh = (hw >> 12) & 1
+key = [(int(xcc[g]), int(se[g, 0]), int(sh[g, 0]), int(cu[g, 0])) for g in range(G)]
+from collections import Counter, defaultdict  # noqa: E402
+by = defaultdict(list)
+for g, k in enumerate(key):
+    by[k].append(g)
+print("  groups per CU: " + str(sorted(Counter(len(v) for v in by.values()).items())))
+pairs = Counter()
+for v in by.values():
+    for i in range(len(v)):
+        for j in range(i + 1, len(v)):
+            a, b = v[i], v[j]
+            for ra in range(4):
+                for rb in range(4):
+                    if simd[a, ra] == simd[b, rb]:
+                        pairs[(roles[ra].split()[0], roles[rb].split()[0])] += 1
+    if len(v) == 2 and len(pairs) < 0:
+        pass
+print("  cross-group SIMD sharing (role pairs): " + ", ".join(f"{a}/{b}:{n}" for (a, b), n in sorted(pairs.items())))
+ex = [v for v in by.values() if len(v) == 2][:4]
+print("  example co-resident groups: " + "; ".join(f"{v[0]}&{v[1]}" for v in ex))

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -67,6 +68,7 @@ struct td_handle {
     uint32_t* d_win = nullptr;
     int win_cap = 0;
     int modulation = 1;                          // td_synth_modulation (MODULATION)
+    int role_cus = 0;                            // CU count for the kernel's role rotation (wg_pos)
     // decoding schedule (td_set_window): window 0 = exact full trellis
     td::WindowParams wp{0, 0, 0, 0, 1.0f};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
@@ -131,6 +133,7 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     dp.lane = h->d_lane;
     dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
     dp.algo = h->p.algo;
+    dp.role_cus = h->role_cus;
 }
 
 // Workspace carve for G groups of the handle's K.
@@ -466,6 +469,10 @@ int td_create(td_handle** out, const td_params* p)
     td_handle* h = new td_handle();
     h->p = *p;
     h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
+    {
+        const char* rot = std::getenv("TD_ROLE_ROT");   // diagnostics: 0 disables the role rotation
+        h->role_cus = (rot && std::atoi(rot) == 0) ? 0 : prop.multiProcessorCount;
+    }
     {
         td::LutEntry<double> l64[td::kLutSize];
         td::LutEntry<float> l32[td::kLutSize];

@@ -47,6 +47,7 @@ struct DecodeParams {
     T* le_dump;                 // nullable
     unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
     int K, L, nT, G, B, iters, all_iters, algo;
+    int role_cus;               // CU count for the second-round role rotation (wg_pos); 0 = off
     int nextstat[kStates][2];
     int laststat[kStates][2];
     int nextout[kStates][4];

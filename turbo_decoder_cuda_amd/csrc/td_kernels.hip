@@ -855,18 +855,25 @@ struct WgPos {
     int g;       // global codeword group index
 };
 
-__device__ __forceinline__ WgPos wg_pos()
+// With one group per workgroup, two workgroups share a CU: blocks b and b + nCU (the second
+// dispatch round), whose wave w lands on the SIMD of the first one's wave w+1.  The second round
+// rotates its roles by 3 so that each recursion wave shares its SIMD with a light role of the other
+// workgroup: A with F0 (the loader), B with F1 (the fold wave, idle in the F pass) -- instead of
+// A with F1 and B with A.  role_cus = the CU count (0: no rotation).
+__device__ __forceinline__ WgPos wg_pos(int role_cus)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
-    return WgPos{h, (wave & 3) ^ (h ? TD_ROLE_XOR : 0), (int)(threadIdx.x & 63), (int)blockIdx.x * kGroupsPerWg + h};
+    const int rot = (kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2) ? 3 : 0;
+    return WgPos{h, ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + rot & 3, (int)(threadIdx.x & 63),
+                 (int)blockIdx.x * kGroupsPerWg + h};
 }
 
 // The whole turbo decode of 8 codewords per workgroup (TurboDecoding, log_map.cpp:1146-1280).
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
 {
-    const WgPos w = wg_pos();
+    const WgPos w = wg_pos(p.role_cus);
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
@@ -894,6 +901,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     }
 #ifdef TD_STAMPS
     st[6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+    st[5] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
     if (p.stamps && lane == 0)
         for (int q = 0; q < kStampSlots; ++q)
             p.stamps[((size_t)w.g * kWaves + wave) * kStampSlots + q] = st[q];
@@ -905,7 +913,7 @@ template <typename T, int ALGO>
 __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
                                                                                           int terminated)
 {
-    const WgPos w = wg_pos();
+    const WgPos w = wg_pos(p.role_cus);
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
