@@ -110,6 +110,40 @@ __global__ void k(double* out, double a, unsigned long long* cyc, int mode)
                 x = x + (double)(q * 8);
             }
             break;
+        case 14:  // alpha step log-MAP: table max* after the group max (the committed kernel's order)
+        case 15:  // alpha step log-MAP: speculative table read from the unnormalised metrics
+        case 16:  // as 15 plus the two per-step global stores of alpha and tempmax
+            {
+                const double sg = (threadIdx.x & 1) ? 1.0 : -1.0, pg = -sg;
+                const double gs = 0.3 * (threadIdx.x & 7), gp = 0.2 * (threadIdx.x & 3);
+                double* st = out + 4096 + blockIdx.x * 64 + threadIdx.x;
+                for (int i = 0; i < N; ++i) {
+                    const double an = dpp<0xB1>(x);
+                    double m = fmax(x, an);
+                    int qu = 0;
+                    double t = 0, l = 0, h = 0;
+                    if (mode != 14) {
+                        const double du = fma(pg, gp, an) - fma(sg, gs, x);
+                        qu = min(max((int)__builtin_amdgcn_ubfe((unsigned)(__double_as_longlong(du) >> 32), 17, 14), 8152), 8152 + 56) - 8152;
+                        t = lds[qu]; l = lds[64 + qu]; h = lds[128 + qu];
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    m = fmax(m, dpp<0x4E>(m));
+                    m = fmax(m, dpp<0x141>(m));
+                    const double al = x - m, ap = an - m;
+                    if (mode == 16) {
+                        asm volatile("global_store_dwordx2 %0, %1, off" :: "v"(st), "v"(al) : "memory");
+                        asm volatile("global_store_dwordx2 %0, %1, off" :: "v"(st + 64 * 64), "v"(m) : "memory");
+                        st += 64 * 64 * 2;
+                    }
+                    const double xs = fma(sg, gs, al), xp = fma(pg, gp, ap);
+                    const double d = xp - xs;
+                    const int q = min(max((int)__builtin_amdgcn_ubfe((unsigned)(__double_as_longlong(d) >> 32), 17, 14), 8152), 8152 + 56) - 8152;
+                    if (mode == 14 || q != qu) { t = lds[q]; l = lds[64 + q]; h = lds[128 + q]; }
+                    x = fmax(xs, xp) + (fabs(d) >= t ? h : l);
+                }
+            }
+            break;
         case 8:   // v_add_f64 pairs interleaved (2 independent chains)
             {
                 double y = x * 0.5;
@@ -130,13 +164,14 @@ int main()
 {
     double* out;
     unsigned long long* cyc;
-    hipMalloc(&out, 64 * 64 * sizeof(double));
+    hipMalloc(&out, (4096 + 64 * 64 * 2 * (N + 1)) * sizeof(double));
     hipMalloc(&cyc, 64 * sizeof(unsigned long long));
     const char* names[] = {"v_add_f64", "v_fma_f64", "v_max_f64+add0", "dpp64+add_f64", "ds_read_b64(idx)+add",
                            "v_add_f32", "gmax3(dpp+max)+add", "int bfe+med3+lshl", "2x add_f64 interleaved",
                            "alpha step maxlog (regs)", "alpha step maxlog (lds g)", "ds_bpermute x2 lookup+add",
-                           "3x ds_read_b64 + sel + add", "bfe+med3+cvt+add"};
-    for (int mode = 0; mode < 14; ++mode) {
+                           "3x ds_read_b64 + sel + add", "bfe+med3+cvt+add",
+                           "alpha logmap (table after max)", "alpha logmap (speculative table)", "alpha logmap spec + 2 stores"};
+    for (int mode = 0; mode < 17; ++mode) {
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);
         hipDeviceSynchronize();
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);

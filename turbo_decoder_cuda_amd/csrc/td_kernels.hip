@@ -92,23 +92,30 @@ __device__ __forceinline__ int bucket_dev<double>(double d)
 {
     const unsigned hi = (unsigned)((unsigned long long)__double_as_longlong(d) >> 32);
     const int q = (int)__builtin_amdgcn_ubfe(hi, BucketBits<double>::shift, BucketBits<double>::width);
-    return min(max(q, BucketBits<double>::base), BucketBits<double>::base + kLutSize - 1) - BucketBits<double>::base;
+    return min(max(q, BucketBits<double>::base), BucketBits<double>::base + kLutSize - 1);
 }
 template <>
 __device__ __forceinline__ int bucket_dev<float>(float d)
 {
     const unsigned b = (unsigned)__float_as_int(d);
     const int q = (int)__builtin_amdgcn_ubfe(b, BucketBits<float>::shift, BucketBits<float>::width);
-    return min(max(q, BucketBits<float>::base), BucketBits<float>::base + kLutSize - 1) - BucketBits<float>::base;
+    return min(max(q, BucketBits<float>::base), BucketBits<float>::base + kLutSize - 1);
 }
 
 // The table lives in LDS as two fields, thr[q] and v[q] (= vlo[q]; vhi[q] = vlo[q+1], see
 // build_lut), each replicated in 16 columns: lane l reads column l % 16, so the 16 lanes an LDS
 // cycle serves always hit 16 distinct bank pairs whatever their buckets (the random buckets of a
 // single shared copy cost ~40% extra LDS cycles in bank conflicts).  `lut` below is the lane's
-// column base (lut_col); vlo[q] and vhi[q] come from one ds_read2_b64.
+// column base shifted down by the first bucket's field value (lut_origin), so that the row address
+// is one lshl_add of the clamped bit field and the three fields are ds_read offsets of it.
 constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last bucket
 constexpr int kLutCols = 16;
+
+template <typename T>
+__device__ __forceinline__ const T* lut_origin(const T* col)
+{
+    return col - BucketBits<T>::base * kLutCols;
+}
 
 template <typename T, int ALGO>
 __device__ __forceinline__ T mstar(T x, T y, const T* lut)
@@ -467,48 +474,36 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
     return StepIn<T>{g[lc.b_sel[PH]], g[lc.b_psel[PH]], tmw[k * kCw + c]};
 }
 
-// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  Streams alpha[.][i] (by state,
-// to `pa`) and the previous step's tempmax (`m_prev`, to `ptm`) to HBM scratch.  The stores are
-// issued while the max* table read is in flight, so they cost the chain nothing; nothing ever
-// waits on them inside the pass.
-//
-// The partner's alpha arrives with the step (`ap`): the next step's partner exchange is the first
-// level of this step's 8-lane max (its mask is one of the three the max needs), taken on the
-// unnormalised metric, and both lanes subtract the codeword's common tempmax themselves --
-// fl(a_partner - tempmax) is exactly the partner's alpha, so the exchange leaves the chain.
-template <int PH>
-struct MaxOrder {   // the 8-lane max's DPP masks, the next phase's partner mask first
-    static constexpr int first = PhaseDpp<(PH + 1) % 3>::ctrl;
-    static constexpr int second = PhaseDpp<(PH + 2) % 3>::ctrl;
-    static constexpr int third = PhaseDpp<PH>::ctrl;
-};
-
+// alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  `a` carries the UNnormalised
+// metric alpha_raw[.][i] of this lane's state; the step takes the reference's tempmax[i] =
+// max_j alpha_raw[j][i] (three DPP levels, the first one the partner exchange of this phase),
+// normalises (:986-1000), streams alpha[.][i] (by state, to `pa`) and tempmax[i] (to `ptm`) to
+// HBM scratch and returns alpha_raw[.][i+1].  fl(an - m) is exactly the partner's normalised
+// alpha, so the exchange is taken on the raw metric, ahead of the max.
+// (A variant that read the max* row of the unnormalised difference ahead of the max, with an
+// exact redo of the window on a bucket mismatch, measured slower: 1098 vs 1203 Mbit/s.)
 template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T alpha_step(T alpha, T& ap, T& m_prev, const StepIn<T>& in, const T* lut,
-                                        const LaneConst<T>& lc, T* pa, T* ptm)
+__device__ __forceinline__ T alpha_step(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc, T* pa, T* ptm)
 {
+    const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw
+    T m = vmax(a, an);
+    m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+    m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
+    const T alpha = a - m, ap = an - m;             // alpha[.][i] of this lane and of the partner
     const T xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
     const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
-    T a;
     if constexpr (ALGO == 1) {
         gstore(pa, alpha);
-        gstore(ptm, m_prev);
-        a = vmax(xs, xp);
+        gstore(ptm, m);
+        return vmax(xs, xp);
     } else {
         const T d = xp - xs;
         const int q = bucket_dev<T>(d);
         const T thr = lut[q * kLutCols], lo = lut[(kLutRows + q) * kLutCols], hi = lut[(kLutRows + q + 1) * kLutCols];
-        gstore(pa, alpha);   // after the table reads in program order: issued in their shadow
-        gstore(ptm, m_prev);
-        a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
+        gstore(pa, alpha);   // in the shadow of the table read
+        gstore(ptm, m);
+        return vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
     }
-    const T an = dpp<MaxOrder<PH>::first>(a);   // the next step's partner, unnormalised
-    T m = vmax(a, an);
-    m = vmax(m, dpp<MaxOrder<PH>::second>(m));
-    m = vmax(m, dpp<MaxOrder<PH>::third>(m));
-    m_prev = m;
-    ap = an - m;
-    return a - m;
 }
 
 // beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  Publishes beta[.][i+1] (by
@@ -533,12 +528,12 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
 }
 
 // alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW.
-// tempmax of step k is stored during step k+1 (index k-1 relative to the step being run); the
-// caller stores the last one.  At t = 0 the first (meaningless) store lands on index 0, which
-// step 1 then overwrites.
+// Step k stores tempmax[i] at scratch index i - 1 (the B pass reads tempmax[i+1] at index i); at
+// t = 0 the first store (tempmax[0]) lands on index 0, which step 1 then overwrites.  The caller
+// stores tempmax[L] after the last window.
 template <typename T, int ALGO>
-__device__ __forceinline__ T alpha_window(T alpha, T& ap, T& m_prev, int t, int n, const Smem<T>& sm, const T* lut,
-                                          int c, const LaneConst<T>& lc, T* ga, T* gtm)
+__device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, const T* lut, int c,
+                                          const LaneConst<T>& lc, T* ga, T* gtm)
 {
     const int tb = t % 3;
     T* pa0 = ga + lc.st_off[0];
@@ -546,26 +541,24 @@ __device__ __forceinline__ T alpha_window(T alpha, T& ap, T& m_prev, int t, int 
     T* pa2 = ga + 2 * kLanes + lc.st_off[2];
     T* ptm = gtm + c - (t > 0 ? kCw : 0);
     int k = 0;
+    StepIn<T> i0 = alpha_in<T, 0>(sm, tb, 0, c, lc);   // operands read one step group ahead
     for (; k + 3 <= n; k += 3) {
-        const StepIn<T> i0 = alpha_in<T, 0>(sm, tb, k, c, lc);
         const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
         const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        alpha = alpha_step<T, ALGO, 0>(alpha, ap, m_prev, i0, lut, lc, pa0 + k * kLanes, ptm);
-        alpha = alpha_step<T, ALGO, 1>(alpha, ap, m_prev, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-        alpha = alpha_step<T, ALGO, 2>(alpha, ap, m_prev, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+        a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+        i0 = alpha_in<T, 0>(sm, tb, min(k + 3, kW - 1), c, lc);
+        a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+        a = alpha_step<T, ALGO, 2>(a, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
         ptm = gtm + c + (k + 2) * kCw;
     }
     if (k < n) {
-        alpha = alpha_step<T, ALGO, 0>(alpha, ap, m_prev, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, pa0 + k * kLanes,
-                                       ptm);
+        a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
         ptm = gtm + c + k * kCw;
     }
     if (k + 1 < n) {
-        alpha = alpha_step<T, ALGO, 1>(alpha, ap, m_prev, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc,
-                                       pa1 + k * kLanes, ptm);
-        ptm = gtm + c + (k + 1) * kCw;
+        a = alpha_step<T, ALGO, 1>(a, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc, pa1 + k * kLanes, ptm);
     }
-    return alpha;
+    return a;
 }
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime)
@@ -685,17 +678,15 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         const int c = lane >> 3;
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
-        T alpha = lc.a_init0 ? (T)0 : (T)-kInfty;   // :943,948
-        T m_prev = (T)0;
-        T ap = dpp<PhaseDpp<0>::ctrl>(alpha);   // the first step's partner
+        T a = lc.a_init0 ? (T)0 : (T)-kInfty;   // alpha[.][0] (:943,948), its tempmax is 0
         __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            alpha = alpha_window<T, ALGO>(alpha, ap, m_prev, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                          ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
+            a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
+                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
             if (t == tl) {
-                gtm0[(size_t)(gm.L - 1) * kCw + c] = m_prev;   // tempmax[L]
+                gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
             }
             TD_STAMP(f1);
@@ -838,7 +829,7 @@ __device__ __forceinline__ void lut_to_lds(const DecodeParams<T>& p, Smem<T>& sm
 template <typename T>
 __device__ __forceinline__ const T* lut_col(const Smem<T>& sm, int lane)
 {
-    return sm.lut + (lane % kLutCols);
+    return lut_origin(sm.lut + (lane % kLutCols));
 }
 
 template <typename T>
@@ -1073,7 +1064,7 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const T* lut = lut_s + (lane % kLutCols);
+    const T* lut = lut_origin(lut_s + (lane % kLutCols));
     // wave -> (decoder, sub-block, 64 codewords); everything but the codeword is wave-uniform
     const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const int cw_waves = a.Bp >> 6, per_dec = a.nS * cw_waves;
