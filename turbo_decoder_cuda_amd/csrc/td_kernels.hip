@@ -102,19 +102,46 @@ __device__ __forceinline__ int bucket_dev<float>(float d)
     return min(max(q, BucketBits<float>::base), BucketBits<float>::base + kLutSize - 1);
 }
 
-// The table lives in LDS as two fields, thr[q] and v[q] (= vlo[q]; vhi[q] = vlo[q+1], see
-// build_lut), each replicated in 16 columns: lane l reads column l % 16, so the 16 lanes an LDS
-// cycle serves always hit 16 distinct bank pairs whatever their buckets (the random buckets of a
-// single shared copy cost ~40% extra LDS cycles in bank conflicts).  `lut` below is the lane's
-// column base shifted down by the first bucket's field value (lut_origin), so that the row address
-// is one lshl_add of the clamped bit field and the three fields are ds_read offsets of it.
+// The table lives in LDS as rows of two fields per bucket, thr[q] and v[q] (= vlo[q]; vhi[q] =
+// vlo[q+1], see build_lut), each field replicated in 16 columns: lane l reads column l % 16, so
+// the 16 lanes an LDS cycle serves always hit 16 distinct bank pairs whatever their buckets (the
+// random buckets of a single shared copy cost ~40% extra LDS cycles in bank conflicts).  Element
+// (q, field f, column) sits at (2q + f) * 16 + column.  A lane's pointer is its column shifted
+// down by the first bucket's bit-field value (lut_origin), so the row address is one lshl_add of
+// the clamped bit field and thr, vlo, vhi are ds_read offsets 0, 128, 384 B of it (one
+// ds_read2 + one ds_read, no address add on the chain).
 constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last bucket
 constexpr int kLutCols = 16;
+constexpr int kLutElems = 2 * kLutRows * kLutCols;
 
 template <typename T>
 __device__ __forceinline__ const T* lut_origin(const T* col)
 {
-    return col - BucketBits<T>::base * kLutCols;
+    return col - 2 * BucketBits<T>::base * kLutCols;
+}
+
+// fill a table copy: element e of the 2 * kLutRows * 16 (one thread per element)
+template <typename T>
+__device__ __forceinline__ T lut_elem(const LutEntry<T>* lut, int e)
+{
+    const int q = e / (2 * kLutCols), f = (e / kLutCols) & 1;
+    if (q >= kLutSize) return f ? (T)lut[kLutSize - 1].vhi : (T)INFINITY;
+    return f ? (T)lut[q].vlo : (T)lut[q].thr;
+}
+
+struct LutRow {
+    int o;   // element offset of the bucket's row from the lane's origin
+};
+template <typename T>
+__device__ __forceinline__ LutRow lut_row(T d)
+{
+    return LutRow{bucket_dev<T>(d) * 2 * kLutCols};
+}
+template <typename T>
+__device__ __forceinline__ T lut_pick(const T* lut, LutRow r, T d)
+{
+    const T thr = lut[r.o], lo = lut[r.o + kLutCols], hi = lut[r.o + 3 * kLutCols];
+    return fabs(d) >= thr ? hi : lo;
 }
 
 template <typename T, int ALGO>
@@ -124,9 +151,7 @@ __device__ __forceinline__ T mstar(T x, T y, const T* lut)
         return vmax(x, y);   // Max-Log-MAP
     } else {
         const T d = y - x;
-        const int q = bucket_dev<T>(d);
-        const T thr = lut[q * kLutCols], lo = lut[(kLutRows + q) * kLutCols], hi = lut[(kLutRows + q + 1) * kLutCols];
-        return vmax(x, y) + (fabs(d) >= thr ? hi : lo);
+        return vmax(x, y) + lut_pick(lut, lut_row(d), d);
     }
 }
 
@@ -202,7 +227,7 @@ constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold
 
 template <typename T>
 struct Smem {
-    T lut[2 * kLutRows * kLutCols];   // max* table: thr[rows][16] | v[rows][16] (see mstar)
+    T lut[kLutElems];   // max* table: [bucket][thr | v][16 columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
     T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
@@ -498,8 +523,8 @@ __device__ __forceinline__ T alpha_step(T a, const StepIn<T>& in, const T* lut, 
         return vmax(xs, xp);
     } else {
         const T d = xp - xs;
-        const int q = bucket_dev<T>(d);
-        const T thr = lut[q * kLutCols], lo = lut[(kLutRows + q) * kLutCols], hi = lut[(kLutRows + q + 1) * kLutCols];
+        const LutRow r = lut_row(d);
+        const T thr = lut[r.o], lo = lut[r.o + kLutCols], hi = lut[r.o + 3 * kLutCols];
         gstore(pa, alpha);   // in the shadow of the table read
         gstore(ptm, m);
         return vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
@@ -569,13 +594,22 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
     T* Bvw = &sm.Bv[xb][0][0];
     const T* tmw = &sm.tm[xb][0][0];
     if (n == kW) {
+        // operands read one step group ahead (the next group's inputs load under this group's chain)
+        StepIn<T> b2 = beta_in<T, 2>(sm, tb, kW - 1, c, lc, tmw);
+        StepIn<T> b1 = beta_in<T, 1>(sm, tb, kW - 2, c, lc, tmw);
+        StepIn<T> b0 = beta_in<T, 0>(sm, tb, kW - 3, c, lc, tmw);
+#pragma unroll
         for (int k = kW - 1; k >= 0; k -= 3) {   // phases 2, 1, 0 (kW = 0 mod 3)
-            const StepIn<T> b2 = beta_in<T, 2>(sm, tb, k, c, lc, tmw);
-            const StepIn<T> b1 = beta_in<T, 1>(sm, tb, k - 1, c, lc, tmw);
-            const StepIn<T> b0 = beta_in<T, 0>(sm, tb, k - 2, c, lc, tmw);
+            const int kn = k >= 3 ? k - 3 : k;
+            const StepIn<T> n2 = beta_in<T, 2>(sm, tb, kn, c, lc, tmw);
+            const StepIn<T> n1 = beta_in<T, 1>(sm, tb, kn - 1, c, lc, tmw);
+            const StepIn<T> n0 = beta_in<T, 0>(sm, tb, kn - 2, c, lc, tmw);
             beta = beta_step<T, ALGO, 2>(beta, b2, lut, k, lc, Bvw);
             beta = beta_step<T, ALGO, 1>(beta, b1, lut, k - 1, lc, Bvw);
             beta = beta_step<T, ALGO, 0>(beta, b0, lut, k - 2, lc, Bvw);
+            b2 = n2;
+            b1 = n1;
+            b0 = n0;
         }
     } else {
         for (int k = n - 1; k >= 0; --k) beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, Bvw, tmw);
@@ -818,12 +852,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
 template <typename T>
 __device__ __forceinline__ void lut_to_lds(const DecodeParams<T>& p, Smem<T>& sm, int tid)
 {
-    for (int e = tid; e < kLutRows * kLutCols; e += kWaves * kLanes) {
-        const int q = e / kLutCols;
-        const bool ok = q < kLutSize;
-        sm.lut[e] = ok ? p.lut[q].thr : (T)INFINITY;
-        sm.lut[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
-    }
+    for (int e = tid; e < kLutElems; e += kWaves * kLanes) sm.lut[e] = lut_elem<T>(p.lut, e);
 }
 
 template <typename T>
@@ -1053,14 +1082,9 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
 template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
-    __shared__ T lut_s[2 * kLutRows * kLutCols];
+    __shared__ T lut_s[kLutElems];
     if constexpr (ALGO == 0) {
-        for (int e = threadIdx.x; e < kLutRows * kLutCols; e += blockDim.x) {
-            const int q = e / kLutCols;
-            const bool ok = q < kLutSize;
-            lut_s[e] = ok ? p.lut[q].thr : (T)INFINITY;
-            lut_s[kLutRows * kLutCols + e] = ok ? p.lut[q].vlo : p.lut[kLutSize - 1].vhi;
-        }
+        for (int e = threadIdx.x; e < kLutElems; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
