@@ -34,15 +34,37 @@ def _run(cmd):
     subprocess.check_call(cmd)
 
 
+def _run_hip(cmd, verbose):
+    """hipcc with the kernel resource report: a kernel that uses scratch is a build error.
+    The turbo kernel's loader counts its vector-memory operations by hand (s_waitcnt vmcnt(N)),
+    and a runtime-indexed array the compiler moved to scratch has also faulted it on the GPU."""
+    cmd = cmd + ["-Rpass-analysis=kernel-resource-usage"]
+    print("+", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    if verbose or r.returncode:
+        sys.stderr.write(r.stderr)
+    if r.returncode:
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    name, bad = None, []
+    for line in r.stderr.splitlines():
+        if "Function Name:" in line:
+            name = line.split("Function Name:")[1].split("[")[0].strip()
+        elif "ScratchSize [bytes/lane]:" in line:
+            n = int(line.split("ScratchSize [bytes/lane]:")[1].split("[")[0])
+            if n:
+                bad.append(f"{name} ({n} B/lane)")
+    if bad:
+        raise RuntimeError("kernels use scratch: " + ", ".join(bad))
+
+
 def build(force: bool = False, verbose: bool = False) -> None:
     srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_synth.hip", "td_api.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
     if force or _newer(LIB, deps):
-        extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose else []
-        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-shared", "-o", LIB, *srcs])
+        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-shared", "-o", LIB, *srcs], verbose)
     stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
     if force or _newer(stamps, deps):
-        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-shared", "-o", stamps, *srcs])
+        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-shared", "-o", stamps, *srcs], False)
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,

@@ -507,49 +507,86 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
 // alpha, so the exchange is taken on the raw metric, ahead of the max.
 // (A variant that read the max* row of the unnormalised difference ahead of the max, with an
 // exact redo of the window on a bucket mismatch, measured slower: 1098 vs 1203 Mbit/s.)
+template <typename T>
+struct StepHalf {   // a recursion step split at its max* table read (see beta_issue)
+    T xs, xp, d, thr, lo, hi;
+};
+
 template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T alpha_step(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc, T* pa, T* ptm)
+__device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc,
+                                                   T* pa, T* ptm)
 {
     const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw
     T m = vmax(a, an);
     m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
     m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
     const T alpha = a - m, ap = an - m;             // alpha[.][i] of this lane and of the partner
-    const T xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
-    const T xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
-    if constexpr (ALGO == 1) {
-        gstore(pa, alpha);
-        gstore(ptm, m);
-        return vmax(xs, xp);
-    } else {
-        const T d = xp - xs;
-        const LutRow r = lut_row(d);
-        const T thr = lut[r.o], lo = lut[r.o + kLutCols], hi = lut[r.o + 3 * kLutCols];
-        gstore(pa, alpha);   // in the shadow of the table read
-        gstore(ptm, m);
-        return vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);   // = mstar(xs, xp)
+    StepHalf<T> h;
+    h.xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
+    h.xp = fma(lc.a_pg[PH], in.gp, ap);      // ... predecessor in the partner lane
+    if constexpr (ALGO == 0) {
+        h.d = h.xp - h.xs;
+        const LutRow r = lut_row(h.d);
+        h.thr = lut[r.o];
+        h.lo = lut[r.o + kLutCols];
+        h.hi = lut[r.o + 3 * kLutCols];
     }
+    gstore(pa, alpha);   // in the shadow of the table read
+    gstore(ptm, m);
+    return h;
 }
 
-// beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  Publishes beta[.][i+1] (by
-// state) for the LLR terms of step i first.
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut, int k,
-                                       const LaneConst<T>& lc, T* Bvw)
+template <typename T, int ALGO>
+__device__ __forceinline__ T step_done(const StepHalf<T>& h)
 {
-    Bvw[k * kLanes + lc.st_off[(PH + 1) % 3]] = beta;
+    if constexpr (ALGO == 1) return vmax(h.xs, h.xp);
+    return vmax(h.xs, h.xp) + (fabs(h.d) >= h.thr ? h.hi : h.lo);   // = mstar(xs, xp)
+}
+
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T alpha_step(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc, T* pa, T* ptm)
+{
+    return step_done<T, ALGO>(alpha_issue<T, ALGO, PH>(a, in, lut, lc, pa, ptm));
+}
+
+// beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  beta[.][i+1] (the incoming
+// metric) is published (by state) for the LLR terms of step i by the caller: an LDS store on the
+// chain costs ~45 cycles a step in isolation (ubench_beta), so a full window may store its 12
+// values at its end (TD_BETA_BATCH).
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc)
+{
     const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
     const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], in.gs, beta), fma(lc.b_pg[PH], in.gp, bp), lut);
     return b - in.tm;
 }
 
+// The same step split at its table read, so that other LDS reads can be issued in its shadow:
+// beta_issue returns once the max* row read is in flight; step_done(h) - tempmax completes it.
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ StepHalf<T> beta_issue(T beta, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc)
+{
+    const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
+    StepHalf<T> h;
+    h.xs = fma(lc.b_sg[PH], in.gs, beta);
+    h.xp = fma(lc.b_pg[PH], in.gp, bp);
+    if constexpr (ALGO == 0) {
+        h.d = h.xp - h.xs;
+        const LutRow r = lut_row(h.d);
+        h.thr = lut[r.o];
+        h.lo = lut[r.o + kLutCols];
+        h.hi = lut[r.o + 3 * kLutCols];
+    }
+    return h;
+}
+
 template <typename T, int ALGO>
 __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, const T* lut, int tb, int k, int c,
-                                          const LaneConst<T>& lc, T* Bvw, const T* tmw)
+                                          const LaneConst<T>& lc, const T* tmw)
 {
-    if (ph == 0) return beta_step<T, ALGO, 0>(beta, beta_in<T, 0>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
-    if (ph == 1) return beta_step<T, ALGO, 1>(beta, beta_in<T, 1>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
-    return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), lut, k, lc, Bvw);
+    if (ph == 0) return beta_step<T, ALGO, 0>(beta, beta_in<T, 0>(sm, tb, k, c, lc, tmw), lut, lc);
+    if (ph == 1) return beta_step<T, ALGO, 1>(beta, beta_in<T, 1>(sm, tb, k, c, lc, tmw), lut, lc);
+    return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), lut, lc);
 }
 
 // alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW.
@@ -567,24 +604,59 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
     T* ptm = gtm + c - (t > 0 ? kCw : 0);
     int k = 0;
     StepIn<T> i0 = alpha_in<T, 0>(sm, tb, 0, c, lc);   // operands read one step group ahead
-    for (; k + 3 <= n; k += 3) {
-        const StepIn<T> i1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
-        const StepIn<T> i2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-        a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
-        i0 = alpha_in<T, 0>(sm, tb, min(k + 3, kW - 1), c, lc);
-        a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-        a = alpha_step<T, ALGO, 2>(a, i2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
-        ptm = gtm + c + (k + 2) * kCw;
+    StepIn<T> i1 = alpha_in<T, 1>(sm, tb, 1, c, lc);
+    if constexpr (ALGO == 1) {
+        // Max-Log-MAP: the next group's reads pinned right behind the group's first step
+        // (1324 -> 1494 Mbit/s); with the table the same placement measured slower (alpha 237 -> 248
+        // cycles a step), so log-MAP keeps the compiler's placement below.
+        StepIn<T> i2 = alpha_in<T, 2>(sm, tb, 2, c, lc);
+        for (; k + 3 <= n; k += 3) {
+            const StepIn<T> c1 = i1, c2 = i2;
+            const int kn = min(k + 3, kW - 3);
+            const StepHalf<T> h = alpha_issue<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+            __builtin_amdgcn_sched_barrier(0);
+            i0 = alpha_in<T, 0>(sm, tb, kn, c, lc);
+            i1 = alpha_in<T, 1>(sm, tb, kn + 1, c, lc);
+            i2 = alpha_in<T, 2>(sm, tb, kn + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            a = step_done<T, ALGO>(h);
+            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+            ptm = gtm + c + (k + 2) * kCw;
+        }
+    } else {
+        for (; k + 3 <= n; k += 3) {
+            const StepIn<T> c1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
+            const StepIn<T> c2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
+            a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+            i0 = alpha_in<T, 0>(sm, tb, min(k + 3, kW - 1), c, lc);
+            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
+            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+            ptm = gtm + c + (k + 2) * kCw;
+        }
+        i1 = alpha_in<T, 1>(sm, tb, min(k + 1, kW - 1), c, lc);
     }
     if (k < n) {
         a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
         ptm = gtm + c + k * kCw;
     }
     if (k + 1 < n) {
-        a = alpha_step<T, ALGO, 1>(a, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc, pa1 + k * kLanes, ptm);
+        a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * kLanes, ptm);
     }
     return a;
 }
+
+#ifndef TD_BETA_BATCH
+#define TD_BETA_BATCH 1
+#endif
+#ifndef TD_BETA_PIN
+#define TD_BETA_PIN 1
+#endif
+constexpr bool kBetaBatch = TD_BETA_BATCH != 0;   // beta published once per window, not per step
+// operand prefetch pinned behind a table read: fp64 only (A/B on one box, config 2: fp64
+// 1192 -> 1207 Mbit/s; fp32 log-MAP 1461 -> 1436, so fp32 keeps the compiler's placement)
+template <typename T>
+constexpr bool kBetaPin = TD_BETA_PIN != 0 && sizeof(T) == 8;
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime)
 template <typename T, int ALGO>
@@ -594,6 +666,13 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
     T* Bvw = &sm.Bv[xb][0][0];
     const T* tmw = &sm.tm[xb][0][0];
     if (n == kW) {
+        T bs[kW];   // beta[.][i+1] of step k, stored by lane after the window (TD_BETA_BATCH)
+        auto put = [&](int k, T v) {
+            if (kBetaBatch)
+                bs[k] = v;
+            else
+                Bvw[k * kLanes + lc.st_off[(k + 1) % 3]] = v;
+        };
         // operands read one step group ahead (the next group's inputs load under this group's chain)
         StepIn<T> b2 = beta_in<T, 2>(sm, tb, kW - 1, c, lc, tmw);
         StepIn<T> b1 = beta_in<T, 1>(sm, tb, kW - 2, c, lc, tmw);
@@ -601,18 +680,32 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
 #pragma unroll
         for (int k = kW - 1; k >= 0; k -= 3) {   // phases 2, 1, 0 (kW = 0 mod 3)
             const int kn = k >= 3 ? k - 3 : k;
+            put(k, beta);
+            const StepHalf<T> h = beta_issue<T, ALGO, 2>(beta, b2, lut, lc);
+            // the next group's operands, issued right behind this step's table read (TD_BETA_PIN)
+            if (kBetaPin<T>) __builtin_amdgcn_sched_barrier(0);
             const StepIn<T> n2 = beta_in<T, 2>(sm, tb, kn, c, lc, tmw);
             const StepIn<T> n1 = beta_in<T, 1>(sm, tb, kn - 1, c, lc, tmw);
             const StepIn<T> n0 = beta_in<T, 0>(sm, tb, kn - 2, c, lc, tmw);
-            beta = beta_step<T, ALGO, 2>(beta, b2, lut, k, lc, Bvw);
-            beta = beta_step<T, ALGO, 1>(beta, b1, lut, k - 1, lc, Bvw);
-            beta = beta_step<T, ALGO, 0>(beta, b0, lut, k - 2, lc, Bvw);
+            if (kBetaPin<T>) __builtin_amdgcn_sched_barrier(0);
+            beta = step_done<T, ALGO>(h) - b2.tm;   // :1019
+            put(k - 1, beta);
+            beta = beta_step<T, ALGO, 1>(beta, b1, lut, lc);
+            put(k - 2, beta);
+            beta = beta_step<T, ALGO, 0>(beta, b0, lut, lc);
             b2 = n2;
             b1 = n1;
             b0 = n0;
         }
+        if (kBetaBatch)
+#pragma unroll
+            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + lc.st_off[(k + 1) % 3]] = bs[k];
     } else {
-        for (int k = n - 1; k >= 0; --k) beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, Bvw, tmw);
+        for (int k = n - 1; k >= 0; --k) {
+            const int ph1 = (k + 1) % 3;   // constant indices only: a runtime index into lc moves it to scratch
+            Bvw[k * kLanes + (ph1 == 0 ? lc.st_off[0] : ph1 == 1 ? lc.st_off[1] : lc.st_off[2])] = beta;
+            beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, tmw);
+        }
     }
     return beta;
 }
@@ -838,8 +931,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = 0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
+#ifndef TD_DIAG_NOFOLD   // diagnostics only: the B pass without its folds (wrong results)
             if (lane < kFoldPerWave && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
+#endif
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -880,13 +975,29 @@ struct WgPos {
 // rotates its roles by 3 so that each recursion wave shares its SIMD with a light role of the other
 // workgroup: A with F0 (the loader), B with F1 (the fold wave, idle in the F pass) -- instead of
 // A with F1 and B with A.  role_cus = the CU count (0: no rotation).
+//
+// TD_ROLE_MAP 1 (measured slower, kept for diagnostics) pairs the roles per SIMD as
+//   S0: B + F0'   S1: F0 + B'   S2: A + F1'   S3: F1 + A'      (' = the second-round workgroup)
+// i.e. wave -> role {B, F0, A, F1} in the first round and {B, F1, A, F0} in the second: in the F
+// pass each alpha chain has its SIMD to itself (F1 idles there), and in the B pass each beta chain
+// shares only with a loader, the two fold waves sharing the remaining SIMDs.
+#ifndef TD_ROLE_MAP
+#define TD_ROLE_MAP 0
+#endif
 __device__ __forceinline__ WgPos wg_pos(int role_cus)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
-    const int rot = (kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2) ? 3 : 0;
-    return WgPos{h, ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + rot & 3, (int)(threadIdx.x & 63),
-                 (int)blockIdx.x * kGroupsPerWg + h};
+    const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
+    int role;
+    if (TD_ROLE_MAP == 1 && kGroupsPerWg == 1) {
+        constexpr unsigned first_map = 1u | (2u << 2) | (0u << 4) | (3u << 6);    // B F0 A F1
+        constexpr unsigned second_map = 1u | (3u << 2) | (0u << 4) | (2u << 6);   // B F1 A F0
+        role = (int)(((second ? second_map : first_map) >> (2 * (wave & 3))) & 3u);
+    } else {
+        role = ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + (second ? 3 : 0) & 3;
+    }
+    return WgPos{h, role, (int)(threadIdx.x & 63), (int)blockIdx.x * kGroupsPerWg + h};
 }
 
 // The whole turbo decode of 8 codewords per workgroup (TurboDecoding, log_map.cpp:1146-1280).
