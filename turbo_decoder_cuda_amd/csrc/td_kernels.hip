@@ -421,10 +421,44 @@ __device__ __forceinline__ void tile_store(const TileRegs<T>& r, Smem<T>& sm, co
 // alpha of window t: HBM scratch -> LDS slot t % 3 directly (global_load_lds_dwordx4, no
 // registers): the window's kW rows are one contiguous 6 KiB block on both sides.  Completion is
 // tracked by vmcnt; the loader waits for it before the barrier that publishes the slot.
-constexpr int kAlphaDma = kW * kLanes * 8 / (kLanes * 16);   // dwordx4 copies per window (fp64)
-constexpr int kAlphaDmaF32 = kW * kLanes * 4 / (kLanes * 16);
+// Max-Log-MAP stores alpha only at the steps of the phases in kCkPhases (i mod 3; phase 0 always)
+// and the folds recompute the steps in between from the last stored one (alpha_recompute): less
+// alpha traffic, which otherwise bounds its forward pass (HBM writes).  The copy gathers the
+// window's stored rows into consecutive LDS rows.
+#ifndef TD_CK_PHASES
+#define TD_CK_PHASES 1   // bit p: alpha of the steps i = p mod 3 is stored (max-log)
+#endif
+constexpr int kCkPhases = TD_CK_PHASES | 1;
+constexpr int kCkPerGroup = (kCkPhases & 1) + ((kCkPhases >> 1) & 1) + ((kCkPhases >> 2) & 1);
+constexpr int kCkRows = kW / 3 * kCkPerGroup;   // stored rows per window
+// window-relative step of stored row r, and the stored row at or before step k (with its step)
+__host__ __device__ constexpr int ck_step(int r)
+{
+    int m = r % kCkPerGroup, p = 0;
+    for (; p < 3; ++p)
+        if ((kCkPhases >> p) & 1) {
+            if (m == 0) break;
+            --m;
+        }
+    return 3 * (r / kCkPerGroup) + p;
+}
+__device__ __forceinline__ int ck_row_of(int k, int& ks)
+{
+    int p = k % 3;
+    while (!((kCkPhases >> p) & 1)) --p;   // phase 0 is always stored
+    ks = k - (k % 3) + p;
+    int m = 0;
+    for (int q = 0; q < p; ++q) m += (kCkPhases >> q) & 1;
+    return (k / 3) * kCkPerGroup + m;
+}
+template <typename T, int ALGO>
+constexpr int alpha_dma_count()
+{
+    return (ALGO == 1 ? kCkRows : kW) * kLanes * (int)sizeof(T) / (kLanes * 16);
+}
+static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
-template <typename T>
+template <typename T, int ALGO>
 __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Geom& gm, int t, int lane)
 {
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
@@ -432,16 +466,20 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     const char* src = reinterpret_cast<const char*>(astore + ((size_t)gm.g * gm.L + (size_t)tc * kW) * kLanes);
     const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(
         &sm.Av[slot][0][0]));
-    constexpr int n = sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32;
+    constexpr int n = alpha_dma_count<T, ALGO>();
+    constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
     // Issued through inline asm (M0 saved and restored around it): with the builtin the compiler
     // guards every later LDS access of this wave with vmcnt(0), as it cannot tell the copy's LDS
     // target from the tile slots, which would serialise the loader on each copy.
 #pragma unroll
     for (int q = 0; q < n; ++q) {
+        // byte b of the copied block: log-MAP rows are the window's steps; max-log row r is step 3r
+        const int b = q * (kLanes * 16) + lane * 16;
+        const int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
         unsigned save;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
                      : "=&s"(save)
-                     : "s"(lds + q * (kLanes * 16)), "v"(src + q * (kLanes * 16) + lane * 16)
+                     : "s"(lds + q * (kLanes * 16)), "v"(src + off)
                      : "memory");
     }
 }
@@ -531,7 +569,7 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
         h.lo = lut[r.o + kLutCols];
         h.hi = lut[r.o + 3 * kLutCols];
     }
-    gstore(pa, alpha);   // in the shadow of the table read
+    if (ALGO == 0 || ((kCkPhases >> PH) & 1)) gstore(pa, alpha);   // in the table read's shadow; max-log: kCkPhases
     gstore(ptm, m);
     return h;
 }
@@ -720,6 +758,23 @@ __device__ __forceinline__ T fold8(const T* v, const T* lut)
     return t;
 }
 
+// Max-Log-MAP alpha step in one lane, all 8 states (:975-1001 with f = 0): the alpha wave's
+// arithmetic exactly -- each state's two candidates alpha[p] -+ (P|Q) (fma(+-1, G, alpha) there),
+// their max, the max over the states (tempmax, exact in any order) and the subtraction.
+template <typename T>
+__device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q)
+{
+    T n[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        n[j] = vmax(a[p0] - (kTrellisQ[p0] ? Q : P), a[p1] + (kTrellisQ[p1] ? Q : P));
+    }
+    const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = n[j] - m;
+}
+
 // LLR fold + extrinsic + outputs of item e = k*8 + c of window t (:1024-1039, :1234-1264):
 //   temp_u[j] = (gamma[p][i][u] + alpha[p][i]) + beta[j][i+1],  p = laststat[j][u],
 //   LLR = E_seq(temp1) - E_seq(temp0)
@@ -734,13 +789,25 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     const T* g = &sm.G[t % 3][k][c][0];
     const T P = g[0], Q = g[1], ys = g[2], la = g[3];
     const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
-    const T* av = &sm.Av[t % kAvSlots][k][c * 8];
-    const T* bv = &sm.Bv[t & 1][k][c * 8];
     T a[8], b[8], t0[8], t1[8];
+    const T* bv = &sm.Bv[t & 1][k][c * 8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        a[j] = av[j];
-        b[j] = bv[j];
+    for (int j = 0; j < 8; ++j) b[j] = bv[j];
+    if constexpr (ALGO == 1) {
+        // alpha[.][i] from the last stored step ks <= k, recomputed through the steps in between
+        // exactly as the alpha wave computed them (:975-1001)
+        int ks;
+        const T* av = &sm.Av[t % kAvSlots][ck_row_of(k, ks)][c * 8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = av[j];
+        for (int s = ks; s < k; ++s) {
+            const T* gs = &sm.G[t % 3][s][c][0];
+            alpha_recompute<T>(a, gs[0], gs[1]);
+        }
+    } else {
+        const T* av = &sm.Av[t % kAvSlots][k][c * 8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = av[j];
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -748,13 +815,20 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
         t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
         t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
     }
-    // the two folds advanced in lock step (independent chains: twice the latency hidden)
-    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
-    T r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
+    T r0, r1;
+    if constexpr (ALGO == 1) {
+        // Max-Log-MAP: E_seq is a plain max, exact in any order -- a tree of depth 3, not 7
+        r0 = vmax(vmax(vmax(t0[0], t0[1]), vmax(t0[2], t0[3])), vmax(vmax(t0[4], t0[5]), vmax(t0[6], t0[7])));
+        r1 = vmax(vmax(vmax(t1[0], t1[1]), vmax(t1[2], t1[3])), vmax(vmax(t1[4], t1[5]), vmax(t1[6], t1[7])));
+    } else {
+        // the two folds advanced in lock step (independent chains: twice the latency hidden)
+        r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
+        r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
 #pragma unroll
-    for (int j = 2; j < 8; ++j) {
-        r0 = mstar<T, ALGO>(r0, t0[j], lut);
-        r1 = mstar<T, ALGO>(r1, t1[j], lut);
+        for (int j = 2; j < 8; ++j) {
+            r0 = mstar<T, ALGO>(r0, t0[j], lut);
+            r1 = mstar<T, ALGO>(r1, t1[j], lut);
+        }
     }
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
@@ -860,7 +934,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // unconditional (clamped windows, a spare slot at the tail), so the per-iteration count kB
         // is fixed and every iteration ends leaving only its own and the previous iteration's issues
         // in flight: three windows of latency for the loads, three for the copies.
-        constexpr int kB = kTileLoads + 1 + (sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32);
+        constexpr int kB = kTileLoads + 1 + alpha_dma_count<T, ALGO>();
         vm_wait<0>();   // the F pass's last (unused) tile loads
         TileRegs<T> ts2;
         TmRegs<T> ms0, ms1, ms2;
@@ -873,7 +947,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             if (wa >= 0) tm_store(ms, sm, wa, lane);
             tile_issue(ts, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
             tm_issue(ms, tmstore, gm, wa - 3, lane);
-            alpha_dma(sm, astore, gm, wa - 1, lane);
+            alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
             vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
             TD_STAMP(b1);
             wg_sync_lds();
@@ -887,8 +961,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         tm_issue(ms1, tmstore, gm, tl - 1, lane);
         tile_issue(ts2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never stored
         tm_issue(ms2, tmstore, gm, tl - 2, lane);
-        alpha_dma(sm, astore, gm, tl, lane);                   // folded at j = 2
-        vm_wait<2 * (kTileLoads + 1) + (sizeof(T) == 8 ? kAlphaDma : kAlphaDmaF32)>();   // set 0 arrived
+        alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);          // folded at j = 2
+        vm_wait<2 * (kTileLoads + 1) + alpha_dma_count<T, ALGO>()>();   // set 0 arrived
         for (int j = 0; j < nB; j += 3) {
             bstep(j, ts0, ms0);
             if (j + 1 < nB) bstep(j + 1, ts1, ms1);
