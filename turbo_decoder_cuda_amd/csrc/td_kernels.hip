@@ -569,7 +569,11 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
         h.lo = lut[r.o + kLutCols];
         h.hi = lut[r.o + 3 * kLutCols];
     }
+#ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
+    if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
+#else
     if (ALGO == 0 || ((kCkPhases >> PH) & 1)) gstore(pa, alpha);   // in the table read's shadow; max-log: kCkPhases
+#endif
     gstore(ptm, m);
     return h;
 }
