@@ -46,3 +46,21 @@ def test_turbo_vs_reference(path):
         ob, ol = O.turbo_decode(d["flow"][fr], K, int(d["f1"]), int(d["f2"]), it)
         assert np.array_equal(out[fr], ob)
         assert np.abs(le[fr] - ol).max() <= LE_TOL_ORACLE
+
+
+@pytest.mark.parametrize("terminated", [1, 0])
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_siso_maxlog_vs_oracle(terminated, precision):
+    """The standalone SISO (Log_MAP_decoder) in Max-Log-MAP, whose folds recompute alpha between
+    the stored rows: LLRs against the oracle's max-log SISO on random channel values and a-priori,
+    several windows long and ragged (L = 1027)."""
+    rng = np.random.default_rng(11 + terminated)
+    L = 1027
+    recs = rng.normal(0.0, 2.0, 2 * L)
+    La = rng.normal(0.0, 3.0, L)
+    c = codec(L - 3, 1, 0, 1, algo="maxlog", precision=precision)
+    llr = c.Log_MAP_decoder(recs.astype(c.dtype), La.astype(c.dtype), terminated)
+    ref = O.siso(recs.astype(c.dtype).astype(np.float64), La.astype(c.dtype).astype(np.float64), terminated,
+                 algo=O.ALGO_MAXLOG)
+    tol = 1e-9 if precision == "f64" else 1e-3 * max(1.0, float(np.abs(ref).max()))
+    assert np.abs(llr - ref).max() <= tol
