@@ -1041,6 +1041,23 @@ __device__ __forceinline__ Smem<T>* smem()
     return reinterpret_cast<Smem<T>*>(td_smem);
 }
 
+// VALU issue priority of the beta wave (ties on a SIMD go to the higher priority, then the older
+// wave).  TD_BETA_PRIO_F32 / _F64 override the default 2 (beta first) per precision.
+#ifndef TD_BETA_PRIO_F64
+#define TD_BETA_PRIO_F64 2
+#endif
+#ifndef TD_BETA_PRIO_F32
+#define TD_BETA_PRIO_F32 0   // fp32: the folds, not beta, bound the B pass (1430 -> 1451 Mbit/s)
+#endif
+template <typename T>
+__device__ __forceinline__ void set_beta_prio()
+{
+    if constexpr (sizeof(T) == 8)
+        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F64);
+    else
+        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F32);
+}
+
 struct WgPos {
     int group;   // codeword group within the workgroup
     int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
@@ -1086,7 +1103,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
-    if (wave == 1) __builtin_amdgcn_s_setprio(2);   // beta first; alpha raises itself in the F pass
+    if (wave == 1) set_beta_prio<T>();   // beta first; alpha raises itself in the F pass
     __syncthreads();
 
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
@@ -1126,7 +1143,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
-    if (wave == 1) __builtin_amdgcn_s_setprio(2);
+    if (wave == 1) set_beta_prio<T>();
     __syncthreads();
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
