@@ -1474,7 +1474,14 @@ hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const 
 }
 
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
-// batch-interleaved arrays.  One thread per (group, step, codeword).
+// batch-interleaved arrays, in two passes:
+//   demux_kernel       one thread per (group, step, codeword): sys1, par1, par2 and the tail rows
+//                      of sys2, straight from the stream (each wave reads 8 codewords x 8 steps);
+//   demux_perm_kernel  sys2[g][i][.] = sys1[g][pi(i)][.] for i < K: SISO2's systematic input is
+//                      SISO1's interleaved (:1109-1113), the same 0.5-scaled value.  Each 8-lane
+//                      group reads one 64-B row, and all blocks of a codeword group run on one XCD
+//                      (blocks go to XCDs round-robin), so the group's 393 KB of sys1 is gathered
+//                      from that XCD's L2 instead of from HBM 8 bytes at a time.
 template <typename T>
 __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* __restrict__ flow)
 {
@@ -1486,7 +1493,7 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
         const int i = (int)(gi % L);
         const int g = (int)(gi / L);
         const int b = g * kCw + c;
-        T ys1 = 0, yp1 = 0, ys2 = 0, yp2 = 0;
+        T ys1 = 0, yp1 = 0, yp2 = 0;
         if (b < p.B) {
             const T* r = flow + (size_t)b * n;
             const T h = (T)0.5;
@@ -1494,20 +1501,34 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
                 ys1 = r[3 * i] * h;
                 yp1 = r[3 * i + 1] * h;
                 yp2 = r[3 * i + 2] * h;
-                ys2 = r[3 * p.pi[i]] * h;
             } else {
                 const int j = i - K;
                 ys1 = r[3 * K + 2 * j] * h;
                 yp1 = r[3 * K + 2 * j + 1] * h;
-                ys2 = r[3 * K + 2 * kMemory + 2 * j] * h;
+                p.sys2[e] = r[3 * K + 2 * kMemory + 2 * j] * h;
                 yp2 = r[3 * K + 2 * kMemory + 2 * j + 1] * h;
             }
+        } else if (i >= K) {
+            p.sys2[e] = 0;
         }
         p.sys1[e] = ys1;
         p.par1[e] = yp1;
-        p.sys2[e] = ys2;
         p.par2[e] = yp2;
     }
+}
+
+constexpr int kPermBlock = 256;
+template <typename T>
+__global__ __launch_bounds__(kPermBlock) void demux_perm_kernel(DecodeParams<T> p, int blocks_per_group)
+{
+    const int b = blockIdx.x;
+    const int xcd = b % 8, r = b / 8;                              // XCD-major: group g on XCD g % 8
+    const int g = (r / blocks_per_group) * 8 + xcd;
+    const int e = (r % blocks_per_group) * kPermBlock + (int)threadIdx.x;   // (step, codeword) in the group
+    if (g >= p.G || e >= p.K * kCw) return;
+    const int i = e >> 3, c = e & 7;
+    const size_t row = (size_t)g * p.L;
+    p.sys2[(row + i) * kCw + c] = p.sys1[(row + p.pi[i]) * kCw + c];
 }
 
 // Bare-SISO input transpose: recs[B][2L] / La[B][L] -> [G][L][8]
@@ -1594,6 +1615,11 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
     int gblocks = (int)((total + 255) / 256);
     if (gblocks > 8192) gblocks = 8192;
     hipLaunchKernelGGL(demux_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, flow);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int bpg = (p.K * kCw + kPermBlock - 1) / kPermBlock;
+    const long long pblocks = (long long)((p.G + 7) / 8) * 8 * bpg;
+    hipLaunchKernelGGL(demux_perm_kernel<T>, dim3((unsigned)pblocks), dim3(kPermBlock), 0, st, p, bpg);
     return hipGetLastError();
 }
 
