@@ -51,6 +51,7 @@ struct td_handle {
     int* d_pinv = nullptr;
     void* d_lut = nullptr;
     td::LaneTables* d_lane = nullptr;
+    unsigned* d_slots = nullptr;   // per-CU occupancy bits of the turbo kernel (wg_pos)
     void* d_ws = nullptr;   // decode workspace
     size_t ws_bytes = 0;
     int ws_groups = 0;
@@ -134,6 +135,7 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
     dp.algo = h->p.algo;
     dp.role_cus = h->role_cus;
+    dp.cu_slots = h->d_slots;
 }
 
 // Workspace carve for G groups of the handle's K.
@@ -491,11 +493,13 @@ int td_create(td_handle** out, const td_params* p)
     if (hipMalloc(&h->d_pi, sizeof(int) * p->K) != hipSuccess ||
         hipMalloc(&h->d_pinv, sizeof(int) * p->K) != hipSuccess ||
         hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess ||
-        hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess) {
+        hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess ||
+        hipMalloc(&h->d_slots, sizeof(unsigned) * td::kCuSlotKeys) != hipSuccess) {
         td_destroy(h);
         return fail(TD_ENOMEM, "td_create: hipMalloc failed");
     }
     hipError_t e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->d_slots, 0, sizeof(unsigned) * td::kCuSlotKeys);
     if (e == hipSuccess) e = hipMemcpy(h->d_lane, &h->lane, sizeof(td::LaneTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         std::vector<int> inv(p->K);
@@ -530,6 +534,7 @@ int td_destroy(td_handle* h)
     if (h->d_pinv) (void)hipFree(h->d_pinv);
     if (h->d_lut) (void)hipFree(h->d_lut);
     if (h->d_lane) (void)hipFree(h->d_lane);
+    if (h->d_slots) (void)hipFree(h->d_slots);
     if (h->d_win) (void)hipFree(h->d_win);
     if (h->d_wws) (void)hipFree(h->d_wws);
     for (auto& tri : h->ev)

@@ -29,6 +29,8 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
+constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
+
 template <typename T>
 struct DecodeParams {
     T* sys1;   // [G][L][8] systematic of decoder 1 (x0.5)
@@ -48,6 +50,7 @@ struct DecodeParams {
     unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
     int K, L, nT, G, B, iters, all_iters, algo;
     int role_cus;               // CU count for the second-round role rotation (wg_pos); 0 = off
+    unsigned* cu_slots;         // [kCuSlotKeys] per-CU occupancy bits (placement-based roles, wg_pos)
     int nextstat[kStates][2];
     int laststat[kStates][2];
     int nextout[kStates][4];

@@ -1063,6 +1063,8 @@ struct WgPos {
     int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
     int lane;
     int g;       // global codeword group index
+    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (2: none)
+    int slot;
 };
 
 // With one group per workgroup, two workgroups share a CU: blocks b and b + nCU (the second
@@ -1076,13 +1078,45 @@ struct WgPos {
 // i.e. wave -> role {B, F0, A, F1} in the first round and {B, F1, A, F0} in the second: in the F
 // pass each alpha chain has its SIMD to itself (F1 idles there), and in the B pass each beta chain
 // shares only with a loader, the two fold waves sharing the remaining SIMDs.
+//
+// TD_ROLE_MAP 2 (default) makes the pairing independent of the dispatcher: the waves read their
+// SIMD from HW_ID and the workgroup takes a free slot (0 or 1) of its CU in a per-CU occupancy
+// word (atomicOr; released at the end, wg_release); role = SIMD for slot 0 and SIMD ^ 2 for slot
+// 1, which gives the pairs A/F0, B/F1 on every SIMD whatever order the workgroups arrived in
+// (a preceding kernel with many small blocks shifted the round-based placement: +4 % kernel time).
+// If two waves of the workgroup share a SIMD, the wave index stands in for the SIMD.
 #ifndef TD_ROLE_MAP
-#define TD_ROLE_MAP 0
+#define TD_ROLE_MAP 2
 #endif
-__device__ __forceinline__ WgPos wg_pos(int role_cus)
+__device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = (int)blockIdx.x * kGroupsPerWg + h;
+    if (TD_ROLE_MAP == 2 && kGroupsPerWg == 1 && role_cus > 0 && slots) {
+        __shared__ int s_simd[kWaves];
+        __shared__ int s_slot;
+        const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+        const int simd = (int)((hw >> 4) & 3);
+        const int key = (int)((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
+        if (threadIdx.x == 0) {
+            int slot = 0;
+            if (atomicOr(&slots[key], 1u) & 1u) slot = (atomicOr(&slots[key], 2u) & 2u) ? 2 : 1;
+            s_slot = slot;
+        }
+        if (lane == 0) s_simd[wave] = simd;
+        __syncthreads();
+        bool distinct = true;
+#pragma unroll
+        for (int a = 0; a < kWaves; ++a)
+#pragma unroll
+            for (int b = a + 1; b < kWaves; ++b) distinct = distinct && s_simd[a] != s_simd[b];
+        const int slot = s_slot;
+        const int base = distinct ? simd : wave;
+        return WgPos{h, slot == 1 ? base ^ 2 : base, lane, g, key, slot};
+    }
     const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
     int role;
     if (TD_ROLE_MAP == 1 && kGroupsPerWg == 1) {
@@ -1092,14 +1126,23 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus)
     } else {
         role = ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + (second ? 3 : 0) & 3;
     }
-    return WgPos{h, role, (int)(threadIdx.x & 63), (int)blockIdx.x * kGroupsPerWg + h};
+    return WgPos{h, role, lane, g, 0, 2};
+}
+
+// end of the kernel: give the CU slot back (all waves of the workgroup are past their work)
+__device__ __forceinline__ void wg_release(const WgPos& w, unsigned* slots)
+{
+    if (w.slot < 2) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicAnd(&slots[w.slot_key], ~(1u << w.slot));
+    }
 }
 
 // The whole turbo decode of 8 codewords per workgroup (TurboDecoding, log_map.cpp:1146-1280).
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
 {
-    const WgPos w = wg_pos(p.role_cus);
+    const WgPos w = wg_pos(p.role_cus, p.cu_slots);
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
@@ -1132,6 +1175,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
         for (int q = 0; q < kStampSlots; ++q)
             p.stamps[((size_t)w.g * kWaves + wave) * kStampSlots + q] = st[q];
 #endif
+    wg_release(w, p.cu_slots);
 }
 
 // Standalone SISO (Log_MAP_decoder) over interleaved [G][L][8] inputs.
@@ -1139,7 +1183,7 @@ template <typename T, int ALGO>
 __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
                                                                                           int terminated)
 {
-    const WgPos w = wg_pos(p.role_cus);
+    const WgPos w = wg_pos(p.role_cus, p.cu_slots);
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
@@ -1149,6 +1193,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
     SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0};
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
+    wg_release(w, p.cu_slots);
 }
 
 // ================================================================== sliding-window mode
@@ -1473,6 +1518,17 @@ hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const 
     return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st) : launch_window_algo<T, 0>(p, w, wb, st);
 }
 
+#ifndef TD_DEMUX_PERM
+#define TD_DEMUX_PERM 1
+#endif
+constexpr bool kDemuxPerm = TD_DEMUX_PERM != 0;   // 0: sys2 gathered from the stream in demux_kernel
+#ifndef TD_PERM_XCD
+#define TD_PERM_XCD 1
+#endif
+#ifndef TD_PERM_NT
+#define TD_PERM_NT 0
+#endif
+
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
 // batch-interleaved arrays, in two passes:
 //   demux_kernel       one thread per (group, step, codeword): sys1, par1, par2 and the tail rows
@@ -1501,6 +1557,7 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
                 ys1 = r[3 * i] * h;
                 yp1 = r[3 * i + 1] * h;
                 yp2 = r[3 * i + 2] * h;
+                if (!kDemuxPerm) p.sys2[e] = r[3 * p.pi[i]] * h;
             } else {
                 const int j = i - K;
                 ys1 = r[3 * K + 2 * j] * h;
@@ -1508,7 +1565,7 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
                 p.sys2[e] = r[3 * K + 2 * kMemory + 2 * j] * h;
                 yp2 = r[3 * K + 2 * kMemory + 2 * j + 1] * h;
             }
-        } else if (i >= K) {
+        } else if (i >= K || !kDemuxPerm) {
             p.sys2[e] = 0;
         }
         p.sys1[e] = ys1;
@@ -1522,13 +1579,22 @@ template <typename T>
 __global__ __launch_bounds__(kPermBlock) void demux_perm_kernel(DecodeParams<T> p, int blocks_per_group)
 {
     const int b = blockIdx.x;
+#if TD_PERM_XCD
     const int xcd = b % 8, r = b / 8;                              // XCD-major: group g on XCD g % 8
     const int g = (r / blocks_per_group) * 8 + xcd;
     const int e = (r % blocks_per_group) * kPermBlock + (int)threadIdx.x;   // (step, codeword) in the group
+#else
+    const int g = b / blocks_per_group;
+    const int e = (b % blocks_per_group) * kPermBlock + (int)threadIdx.x;
+#endif
     if (g >= p.G || e >= p.K * kCw) return;
     const int i = e >> 3, c = e & 7;
     const size_t row = (size_t)g * p.L;
+#if TD_PERM_NT
+    __builtin_nontemporal_store(p.sys1[(row + p.pi[i]) * kCw + c], &p.sys2[(row + i) * kCw + c]);
+#else
     p.sys2[(row + i) * kCw + c] = p.sys1[(row + p.pi[i]) * kCw + c];
+#endif
 }
 
 // Bare-SISO input transpose: recs[B][2L] / La[B][L] -> [G][L][8]
@@ -1617,6 +1683,7 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
     hipLaunchKernelGGL(demux_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, flow);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (!kDemuxPerm) return hipSuccess;
     const int bpg = (p.K * kCw + kPermBlock - 1) / kPermBlock;
     const long long pblocks = (long long)((p.G + 7) / 8) * 8 * bpg;
     hipLaunchKernelGGL(demux_perm_kernel<T>, dim3((unsigned)pblocks), dim3(kPermBlock), 0, st, p, bpg);
