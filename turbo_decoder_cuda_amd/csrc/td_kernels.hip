@@ -1042,17 +1042,23 @@ __device__ __forceinline__ Smem<T>* smem()
 }
 
 // VALU issue priority of the beta wave (ties on a SIMD go to the higher priority, then the older
-// wave).  TD_BETA_PRIO_F32 / _F64 override the default 2 (beta first) per precision.
+// wave).  Log-MAP fp64: beta bounds the B pass, so it goes first (2).  fp32 log-MAP and Max-Log-MAP:
+// the folds bound the B pass and beta yields (0).  TD_BETA_PRIO_* override.
 #ifndef TD_BETA_PRIO_F64
 #define TD_BETA_PRIO_F64 2
 #endif
 #ifndef TD_BETA_PRIO_F32
 #define TD_BETA_PRIO_F32 0   // fp32: the folds, not beta, bound the B pass (1430 -> 1451 Mbit/s)
 #endif
-template <typename T>
+#ifndef TD_BETA_PRIO_MAXLOG
+#define TD_BETA_PRIO_MAXLOG 0
+#endif
+template <typename T, int ALGO>
 __device__ __forceinline__ void set_beta_prio()
 {
-    if constexpr (sizeof(T) == 8)
+    if constexpr (ALGO == 1)
+        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_MAXLOG);
+    else if constexpr (sizeof(T) == 8)
         __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F64);
     else
         __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F32);
@@ -1146,7 +1152,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
-    if (wave == 1) set_beta_prio<T>();   // beta first; alpha raises itself in the F pass
+    if (wave == 1) set_beta_prio<T, ALGO>();   // beta first; alpha raises itself in the F pass
     __syncthreads();
 
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
@@ -1187,7 +1193,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     Smem<T>& sm = smem<T>()[w.group];
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
-    if (wave == 1) set_beta_prio<T>();
+    if (wave == 1) set_beta_prio<T, ALGO>();
     __syncthreads();
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
