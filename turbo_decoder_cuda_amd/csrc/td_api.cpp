@@ -290,7 +290,8 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     const size_t eA = ((size_t)G * L + td::window_steps()) * 64 * sizeof(T);
     const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
     char* buf = nullptr;
-    const size_t eP = (size_t)L * sizeof(int);   // zero permutation tables: the bare SISO writes no extrinsic
+    // zero permutation tables (the bare SISO writes no extrinsic), with the loader's spare ints
+    const size_t eP = ((size_t)L + td::kPermPad) * sizeof(int);
     const size_t total = 5 * align_up(eL, 256) + align_up(eA, 256) + align_up(inR, 256) + 2 * align_up(inA, 256) +
                          align_up(eP, 256);
     if (hipMalloc(&buf, total) != hipSuccess) return fail(TD_ENOMEM, "hipMalloc (siso) failed");
@@ -490,15 +491,18 @@ int td_create(td_handle** out, const td_params* p)
         return fail(TD_EINVAL, "td_create: trellis does not fit the rotating-label kernel");
     }
     h->pi = std::move(pi);
-    if (hipMalloc(&h->d_pi, sizeof(int) * p->K) != hipSuccess ||
-        hipMalloc(&h->d_pinv, sizeof(int) * p->K) != hipSuccess ||
+    // the permutation tables carry td::kPermPad spare (zero) ints: the loader stages whole windows
+    if (hipMalloc(&h->d_pi, sizeof(int) * (p->K + td::kPermPad)) != hipSuccess ||
+        hipMalloc(&h->d_pinv, sizeof(int) * (p->K + td::kPermPad)) != hipSuccess ||
         hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess ||
         hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess ||
         hipMalloc(&h->d_slots, sizeof(unsigned) * td::kCuSlotKeys) != hipSuccess) {
         td_destroy(h);
         return fail(TD_ENOMEM, "td_create: hipMalloc failed");
     }
-    hipError_t e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
+    hipError_t e = hipMemset(h->d_pi, 0, sizeof(int) * (p->K + td::kPermPad));
+    if (e == hipSuccess) e = hipMemset(h->d_pinv, 0, sizeof(int) * (p->K + td::kPermPad));
+    if (e == hipSuccess) e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(h->d_slots, 0, sizeof(unsigned) * td::kCuSlotKeys);
     if (e == hipSuccess) e = hipMemcpy(h->d_lane, &h->lane, sizeof(td::LaneTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) {

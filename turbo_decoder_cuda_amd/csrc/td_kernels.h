@@ -29,6 +29,7 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
+constexpr int kPermPad = 16;         // spare ints after pi / pinv: the loader stages window-sized chunks
 constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
 
 template <typename T>

@@ -225,6 +225,19 @@ constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (
 static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 
+// Loader staging.  Window inputs travel HBM -> LDS by DMA (global_load_lds_dwordx4: no VGPR
+// destination, completion counted by vmcnt; LDS target = wave-uniform base + 16 * lane) and the
+// loader then converts a landed slot into the ring.  A staged window is 16-byte chunks: ys, yp, La
+// ([kW][8] each), then the write positions pi-or-pinv[kW] and pi[kW]; spare lanes land past them.
+constexpr int kDmaBytes = kLanes * 16;   // one DMA instruction
+static_assert(kW % 4 == 0, "a window's write positions are whole 16-byte chunks");
+template <typename T>
+constexpr int kStreamChunks = kTile * (int)sizeof(T) / 16;   // chunks of one [kW][8] stream
+template <typename T>
+constexpr int kTileChunks = 3 * kStreamChunks<T> + 2 * (kW / 4);
+template <typename T>
+constexpr int kTileDma = (kTileChunks<T> + kLanes - 1) / kLanes;   // DMA instructions per staged window
+
 template <typename T>
 struct Smem {
     T lut[kLutElems];   // max* table: [bucket][thr | v][16 columns] (see lut_origin)
@@ -233,6 +246,8 @@ struct Smem {
     T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
+    alignas(16) unsigned char stage[3][kTileDma<T> * kDmaBytes];   // loader: staged window inputs
+    alignas(16) unsigned char tmstage[3][kDmaBytes];                // loader: staged tempmax of a window
 };
 
 // raw barrier: waits for this wave's LDS traffic only, so prefetched global loads stay in flight
@@ -298,39 +313,7 @@ __device__ __forceinline__ T la_at(const SisoSrc<T>& src, int i, T raw)
     return i < src.la_len ? raw : (T)0;
 }
 
-// ---- tile loader (wave F0): element e = lane and e = lane + 64 (< kTile) of a window
-constexpr int kLoadPerLane = (kTile + kLanes - 1) / kLanes;   // 2
-
-// ---- loader global loads: explicit instructions with hand-counted vmcnt waits.  The compiler
-// sees these loads as completed at issue, so it inserts no waits of its own (its conservative
-// merging across the two-set pipeline drained the whole queue every window); the loader waits
-// with vm_wait<N>() and then "touches" the set so no use can be scheduled above the wait.
-__device__ __forceinline__ void gload(double& d, const double* p)
-{
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-__device__ __forceinline__ void gload(float& d, const float* p)
-{
-    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-__device__ __forceinline__ void gload(int& d, const int* p)
-{
-    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-__device__ __forceinline__ void gload2(double& a, double& b, const double* p)   // one 16-byte load
-{
-    double2 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    a = v.x;
-    b = v.y;
-}
-__device__ __forceinline__ void gload2(float& a, float& b, const float* p)
-{
-    float2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    a = v.x;
-    b = v.y;
-}
+// ---- loader helpers
 template <int N>
 __device__ __forceinline__ void vm_wait()
 {
@@ -352,69 +335,112 @@ __device__ __forceinline__ void gstore(float* p, float v)
     asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 
-template <typename T>
-struct TileRegs {
-    T ys[kLoadPerLane], yp[kLoadPerLane], la[kLoadPerLane];
-    int wperm[kLoadPerLane], wbit[kLoadPerLane];
-};
-constexpr int kTileLoads = kLoadPerLane * 5;   // vector-memory instructions per tile_issue
-
-template <typename T>
-__device__ __forceinline__ void touch(TileRegs<T>& r)
+__device__ __forceinline__ unsigned lds_addr(const void* p)
 {
+    return (unsigned)(size_t)(__attribute__((address_space(3))) const char*)(reinterpret_cast<const char*>(p));
+}
+// One 16-byte chunk per lane, HBM -> LDS at lds + 16 * lane.  Issued through inline asm (M0 saved
+// and restored around it): with the builtin the compiler guards every later LDS access of this
+// wave with vmcnt(0), as it cannot tell the DMA's LDS target from the other LDS arrays, which would
+// serialise the loader on each copy.  The loader waits for completion with vm_wait<N>() before the
+// barrier that publishes the slot (or before reading the slot itself).
+__device__ __forceinline__ void dma16(unsigned lds, const void* src)
+{
+    unsigned save;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "s"(lds), "v"(src)
+                 : "memory");
+}
+
+// Stage window t (rows clamped into range, so the count of DMA instructions never varies; values
+// are masked where they are converted).  Every read is sequential: the interleaver permutations
+// are applied when the extrinsic is WRITTEN (fold), so no load address depends on another load.
+// The write-position chunks read up to 13 ints past K: the permutation tables carry 16 spare ints.
+template <typename T>
+__device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>& src, const SisoDst<T>& dst,
+                                         const Geom& gm, int t, int lane)
+{
+    constexpr int E = 16 / (int)sizeof(T);   // elements per chunk (a chunk never crosses a step row)
+    constexpr int nc = kStreamChunks<T>;
+    const int* pperm = dst.ext_mode == 3 ? gm.pinv : gm.pi;
+    const unsigned base = lds_addr(&sm.stage[slot][0]);
+    const int tc = max(t, 0);
 #pragma unroll
-    for (int q = 0; q < kLoadPerLane; ++q) {
-        touch(r.ys[q]);
-        touch(r.yp[q]);
-        touch(r.la[q]);
-        touch(r.wperm[q]);
-        touch(r.wbit[q]);
+    for (int q = 0; q < kTileDma<T>; ++q) {
+        const int ch = q * kLanes + lane;
+        // stream chunks: s = 0 ys, 1 yp, 2 La
+        const int cs = min(ch, 3 * nc - 1);
+        const int s = cs / nc, e0 = (cs - s * nc) * E;
+        const int i = min(tc * kW + (e0 >> 3), gm.L - 1);
+        // base of stream s by arithmetic (a select chain over the three pointers becomes a
+        // runtime-indexed private array, i.e. scratch)
+        const size_t a0 = (size_t)src.sys, a1 = (size_t)src.par, a2 = (size_t)src.la;
+        const size_t sb = a0 + (size_t)(s == 1) * (a1 - a0) + (size_t)(s == 2) * (a2 - a0);
+        const size_t row = s == 2 ? (size_t)gm.g * src.la_cap + min(i, src.la_cap - 1) : (size_t)gm.g * gm.L + i;
+        const char* ps = reinterpret_cast<const char*>(sb + (row * kCw + (e0 & 7)) * sizeof(T));
+        // write-position chunks: r < kW/4 pi-or-pinv, else pi
+        const int r = min(max(ch - 3 * nc, 0), 2 * (kW / 4) - 1);
+        const int* pb = r < kW / 4 ? pperm : gm.pi;
+        const char* pw = reinterpret_cast<const char*>(pb + tc * kW + (r % (kW / 4)) * 4);
+        dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);   // spare lanes repeat the last chunk
     }
 }
 
-// element e of window t (clamped, so the count of loads never varies); values masked at use
+// tempmax of window t ([kW][8], rows clamped) -> staging slot; one DMA instruction
 template <typename T>
-__device__ __forceinline__ void tile_issue(TileRegs<T>& r, const SisoSrc<T>& src, const SisoDst<T>& dst,
-                                           const Geom& gm, int t, int lane)
+__device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, const Geom& gm, int t, int lane)
 {
-    const int* pperm = dst.ext_mode == 3 ? gm.pinv : gm.pi;
+    constexpr int E = 16 / (int)sizeof(T);
+    const int e0 = min(lane, kStreamChunks<T> - 1) * E;
+    const int i = min(max(t * kW + (e0 >> 3), 0), gm.L - 1);
+    dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
+}
+
+// staged tempmax of window t -> its LDS slot (beta input)
+template <typename T>
+__device__ __forceinline__ void tm_convert(Smem<T>& sm, int slot, int t, int lane)
+{
+    const T* sv = reinterpret_cast<const T*>(&sm.tmstage[slot][0]);
+    T* d = &sm.tm[t & 1][0][0];
 #pragma unroll
-    for (int q = 0; q < kLoadPerLane; ++q) {
-        const int e = min(lane + kLanes * q, kTile - 1);
-        const int k = e >> 3, c = e & 7;
-        const int i = min(max(t * kW + k, 0), gm.L - 1);
-        const size_t off = ((size_t)gm.g * gm.L + i) * kCw + c;
-        gload(r.ys[q], src.sys + off);
-        gload(r.yp[q], src.par + off);
-        gload(r.la[q], src.la + ((size_t)gm.g * src.la_cap + min(i, src.la_cap - 1)) * kCw + c);
-        const int ik = min(i, gm.K - 1);
-        gload(r.wperm[q], pperm + ik);
-        gload(r.wbit[q], gm.pi + ik);
+    for (int q = 0; q < 2; ++q) {
+        const int e = lane + kLanes * q;
+        if (e < kTile) d[e] = sv[e];
     }
 }
 
 // (P, Q) of the four branch metrics (see "gamma"), ys and La for the extrinsic, and the write
-// positions, into the LDS ring slot of window t
+// positions of staged window t, into the LDS ring slot of window t
 template <typename T>
-__device__ __forceinline__ void tile_store(const TileRegs<T>& r, Smem<T>& sm, const SisoSrc<T>& src, int t, int lane)
+__device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int lane)
 {
+    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
+    const T* sp = sy + kTile;
+    const T* sl = sy + 2 * kTile;
+    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile);   // [kW] pi-or-pinv, then [kW] pi
     T* g = &sm.G[t % 3][0][0][0];
     int* w = &sm.Wp[t % 3][0][0][0];
 #pragma unroll
-    for (int q = 0; q < kLoadPerLane; ++q) {
+    for (int q = 0; q < 2; ++q) {
         const int e = lane + kLanes * q;
         if (e < kTile) {
-            const T la = la_at(src, t * kW + (e >> 3), r.la[q]);
+            const int k = e >> 3;
+            const T ys = sy[e], yp = sp[e];
+            const T la = la_at(src, t * kW + k, sl[e]);
             const T hla = la / (T)2;
-            g[4 * e] = (r.ys[q] + r.yp[q]) + hla;
-            g[4 * e + 1] = (r.ys[q] - r.yp[q]) + hla;
-            g[4 * e + 2] = r.ys[q];
+            g[4 * e] = (ys + yp) + hla;
+            g[4 * e + 1] = (ys - yp) + hla;
+            g[4 * e + 2] = ys;
             g[4 * e + 3] = la;
-            w[2 * e] = r.wperm[q];
-            w[2 * e + 1] = r.wbit[q];
+            w[2 * e] = sw[k];
+            w[2 * e + 1] = sw[kW + k];
         }
     }
 }
+static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
+// the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
+static_assert(kMemory + kW - 2 < kPermPad, "write-position chunks stay within the padded tables");
 
 // ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
 // Scratch layout: alpha [g][L][64] by 8c + state, tempmax [g][L][8].
@@ -464,53 +490,15 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
     const char* src = reinterpret_cast<const char*>(astore + ((size_t)gm.g * gm.L + (size_t)tc * kW) * kLanes);
-    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(
-        &sm.Av[slot][0][0]));
+    const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
-    // Issued through inline asm (M0 saved and restored around it): with the builtin the compiler
-    // guards every later LDS access of this wave with vmcnt(0), as it cannot tell the copy's LDS
-    // target from the tile slots, which would serialise the loader on each copy.
 #pragma unroll
     for (int q = 0; q < n; ++q) {
         // byte b of the copied block: log-MAP rows are the window's steps; max-log row r is step 3r
-        const int b = q * (kLanes * 16) + lane * 16;
+        const int b = q * kDmaBytes + lane * 16;
         const int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
-        unsigned save;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(save)
-                     : "s"(lds + q * (kLanes * 16)), "v"(src + off)
-                     : "memory");
-    }
-}
-
-template <typename T>
-struct TmRegs {
-    T v[2];    // elements 2*lane, 2*lane+1 of the window's [kW][8] tempmax block (lanes < 48)
-};
-
-template <typename T>
-__device__ __forceinline__ void tm_issue(TmRegs<T>& r, const T* tmstore, const Geom& gm, int t, int lane)
-{
-    const int e = min(max(t * kW * kCw + 2 * lane, 0), gm.L * kCw - 2);   // clamped: always a valid pair
-    gload2(r.v[0], r.v[1], tmstore + (size_t)gm.g * gm.L * kCw + e);      // one instruction
-}
-
-template <typename T>
-__device__ __forceinline__ void touch(TmRegs<T>& r)
-{
-    touch(r.v[0]);
-    touch(r.v[1]);
-}
-
-template <typename T>
-__device__ __forceinline__ void tm_store(const TmRegs<T>& r, Smem<T>& sm, int t, int lane)
-{
-    const int e = 2 * lane;
-    if (e < kTile) {
-        T* d = &sm.tm[t & 1][0][0] + e;
-        d[0] = r.v[0];
-        d[1] = r.v[1];
+        dma16(lds + q * kDmaBytes, src + off);
     }
 }
 
@@ -902,55 +890,48 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         __builtin_amdgcn_s_setprio(0);   // in the B pass the beta wave goes first
     } else if (wave == 2) {
-        // Loader: two register sets by window parity, unrolled by two so each set is static.
-        // Invariant: at the top of an iteration the set it consumes has fully arrived; every
-        // iteration ends with a wait that leaves only its own issues in flight.
-        // F pass iteration t: store tile t+1, issue tile t+3 (into the same set).
-        TileRegs<T> ts0, ts1;
-        auto fstep = [&](int t, TileRegs<T>& set) {
+        // Loader: every input travels HBM -> LDS by DMA into a staging slot, and this wave converts
+        // landed slots into the ring (no VGPR is ever the target of a load in flight).
+        // Invariant: every iteration ends with a wait that leaves only its own DMAs in flight.
+        // F pass iteration t: convert window t+1 (staged two iterations ago, slot (t+1) % 3) and
+        // stage window t+3 into slot t % 3, which window t left one iteration ago.
+        constexpr int kF = kTileDma<T>;
+        auto fstep = [&](int t) {
             TD_STAMP(f0);
-            touch(set);
-            if (t + 1 <= tl) tile_store(set, sm, src, t + 1, lane);
-            tile_issue(set, src, dst, gm, min(t + 3, tl), lane);
-            vm_wait<kTileLoads>();   // tile t+2 (other set) has arrived
+            if (t + 1 <= tl) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
+            tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
+            vm_wait<kF>();   // window t+2 has landed
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
             TD_ACC(0, f0, f1);
             TD_ACC(1, f1, f2);
         };
-        tile_issue(ts0, src, dst, gm, 0, lane);
+        tile_dma(sm, 0, src, dst, gm, 0, lane);
         vm_wait<0>();
-        touch(ts0);
-        tile_store(ts0, sm, src, 0, lane);
-        tile_issue(ts1, src, dst, gm, min(1, tl), lane);
-        tile_issue(ts0, src, dst, gm, min(2, tl), lane);
-        vm_wait<kTileLoads>();
+        tile_convert(sm, 0, src, 0, lane);
+        tile_dma(sm, 1, src, dst, gm, min(1, tl), lane);
+        tile_dma(sm, 2, src, dst, gm, min(2, tl), lane);
+        vm_wait<kF>();
         wg_sync_lds();
-        for (int t = 0; t < nT; t += 2) {
-            fstep(t, ts1);
-            if (t + 1 < nT) fstep(t + 1, ts0);
-        }
-        // B pass iteration j (wa = tl - j) stores tile wa (tiles tl-2..tl never left the ring) and
-        // tempmax of wa (beta, next iteration) into the LDS slots nobody reads this iteration, issues
-        // the same streams three windows lower into the set it just consumed, and copies alpha of
-        // wa-1 (folded at j+3) straight into LDS slot (wa-1) % 4 (last read at j-1).  All issues are
-        // unconditional (clamped windows, a spare slot at the tail), so the per-iteration count kB
-        // is fixed and every iteration ends leaving only its own and the previous iteration's issues
-        // in flight: three windows of latency for the loads, three for the copies.
-        constexpr int kB = kTileLoads + 1 + alpha_dma_count<T, ALGO>();
-        vm_wait<0>();   // the F pass's last (unused) tile loads
-        TileRegs<T> ts2;
-        TmRegs<T> ms0, ms1, ms2;
-        auto bstep = [&](int j, TileRegs<T>& ts, TmRegs<T>& ms) {
+        for (int t = 0; t < nT; ++t) fstep(t);
+        // B pass iteration j (wa = tl - j) converts the tiles of wa (tiles tl-2..tl never left the
+        // ring) and tempmax of wa (beta, next iteration) from staging slot j % 3 into the LDS slots
+        // nobody reads this iteration, stages the same streams three windows lower into the slot it
+        // just read, and copies alpha of wa-1 (folded at j+3) straight into LDS slot (wa-1) % 4
+        // (last read at j-1).  All DMAs are unconditional (clamped windows, a spare slot at the
+        // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
+        // own and the previous iteration's DMAs in flight: three windows of latency for each.
+        constexpr int kB = kF + 1 + alpha_dma_count<T, ALGO>();
+        vm_wait<0>();   // the F pass's last (unused) staging
+        auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
             const int wa = tl - j;
-            touch(ts);
-            touch(ms);
-            if (wa >= 0 && wa <= tl - 3) tile_store(ts, sm, src, wa, lane);
-            if (wa >= 0) tm_store(ms, sm, wa, lane);
-            tile_issue(ts, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
-            tm_issue(ms, tmstore, gm, wa - 3, lane);
+            if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
+            if (wa >= 0) tm_convert(sm, slot, wa, lane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+            tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+            tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
             alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
             vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
             TD_STAMP(b1);
@@ -959,18 +940,18 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             TD_ACC(2, b0, b1);
             TD_ACC(3, b1, b2);
         };
-        tile_issue(ts0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never stored
-        tm_issue(ms0, tmstore, gm, tl, lane);
-        tile_issue(ts1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never stored
-        tm_issue(ms1, tmstore, gm, tl - 1, lane);
-        tile_issue(ts2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never stored
-        tm_issue(ms2, tmstore, gm, tl - 2, lane);
+        tile_dma(sm, 0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never converted
+        tm_dma(sm, 0, tmstore, gm, tl, lane);
+        tile_dma(sm, 1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never converted
+        tm_dma(sm, 1, tmstore, gm, tl - 1, lane);
+        tile_dma(sm, 2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never converted
+        tm_dma(sm, 2, tmstore, gm, tl - 2, lane);
         alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);          // folded at j = 2
-        vm_wait<2 * (kTileLoads + 1) + alpha_dma_count<T, ALGO>()>();   // set 0 arrived
+        vm_wait<2 * (kF + 1) + alpha_dma_count<T, ALGO>()>();   // slot 0 landed
         for (int j = 0; j < nB; j += 3) {
-            bstep(j, ts0, ms0);
-            if (j + 1 < nB) bstep(j + 1, ts1, ms1);
-            if (j + 2 < nB) bstep(j + 2, ts2, ms2);
+            bstep(j, 0);
+            if (j + 1 < nB) bstep(j + 1, 1);
+            if (j + 2 < nB) bstep(j + 2, 2);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
@@ -1659,24 +1640,34 @@ inline hipError_t allow_smem(const void* fn, size_t bytes)
     return hipSuccess;
 }
 
+// LDS per workgroup: the Smem of its groups, but never less than a third of the CU's 160 KiB, so
+// that at most two workgroups share a CU whatever the kernel's register count (the role pairing
+// per SIMD, wg_pos, and the load balance of B/8 workgroups over 256 CUs assume two).
+constexpr size_t kMinWgLds = 160 * 1024 / 3 + 1024;
+template <typename T>
+constexpr size_t wg_lds()
+{
+    return kGroupsPerWg * sizeof(Smem<T>) > kMinWgLds ? kGroupsPerWg * sizeof(Smem<T>) : kMinWgLds;
+}
+static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
+
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st)
 {
-    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>),
-                              kGroupsPerWg * sizeof(Smem<T>));
+    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>), wg_lds<T>());
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
-                       kGroupsPerWg * sizeof(Smem<T>), st, p);
+                       wg_lds<T>(), st, p);
     return hipGetLastError();
 }
 
 template <typename T, int ALGO>
 hipError_t launch_siso_algo(const DecodeParams<T>& p, const T* la, int terminated, hipStream_t st)
 {
-    hipError_t e = allow_smem(reinterpret_cast<const void*>(&siso_kernel<T, ALGO>), kGroupsPerWg * sizeof(Smem<T>));
+    hipError_t e = allow_smem(reinterpret_cast<const void*>(&siso_kernel<T, ALGO>), wg_lds<T>());
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((siso_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
-                       kGroupsPerWg * sizeof(Smem<T>), st, p, la, terminated);
+                       wg_lds<T>(), st, p, la, terminated);
     return hipGetLastError();
 }
 
