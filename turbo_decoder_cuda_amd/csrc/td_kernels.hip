@@ -201,11 +201,12 @@ __device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneC
 // ------------------------------------------------------------------ workgroup roles
 // One workgroup = 4 waves = 8 codewords.  A SISO is two passes over windows of kW steps:
 //   F pass   wave 0 (A) runs alpha forward and streams alpha (by state) and tempmax of every
-//            step to HBM scratch; wave 2 (F0) loads the (P, Q) tiles two windows ahead.
+//            step to HBM scratch; wave 2 (F0) stages the window inputs by LDS DMA and converts
+//            them into the (P, Q) tiles one window ahead.
 //   B pass   windows last..first, a three-stage pipeline per iteration j (wa = tl - j):
 //            wave 1 (B)   beta over window wa+1 (tempmax from LDS), publishing beta by state;
-//            wave 2 (F0)  tiles of window wa, tempmax of wa, alpha of wa+1: HBM -> LDS, loads
-//                         issued two iterations ahead;
+//            wave 2 (F0)  converts the staged tiles and tempmax of window wa, stages window wa-3
+//                         and copies alpha of wa-1, all HBM -> LDS by DMA;
 //            waves 0, 3   LLR folds of window wa+2 (beta finished last iteration), one (step,
 //                         codeword) item per lane, both input bits in the same lane.
 // Only the two recursions are serial chains; nothing else waits on them but the barriers.  The
