@@ -87,6 +87,8 @@ def main():
 
     if world > 1:
         dist.init_process_group(backend="gloo")
+    # one GPU per rank; more ranks than GPUs (a rehearsal on a smaller box) share them round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     f1, f2 = qpp_for(a.K)
