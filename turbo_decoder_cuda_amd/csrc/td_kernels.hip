@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "td_kernels.h"
 #include "td_tables.h"
@@ -250,6 +251,56 @@ struct Smem {
     alignas(16) unsigned char stage[3][kTileDma<T> * kDmaBytes];   // loader: staged window inputs
     alignas(16) unsigned char tmstage[3][kDmaBytes];                // loader: staged tempmax of a window
 };
+
+// Fold-input rows (Av, Bv): a (row, codeword) block holds the 8 states, 64 B in fp64 (4 chunks of
+// 16 B), 32 B in fp32 (2 chunks).  A fold lane reads its whole block one 16-B chunk per
+// ds_read_b128; with the blocks unrotated, the 16 lanes of a read group hit only 4 (fp64) or 8
+// (fp32) distinct bank slots, a 4- or 2-way conflict.  Chunk p of the block in row r is stored at
+// chunk (p + r) mod (chunks per block): the lane of row r then reads chunk p at slot
+// 4c + ((p + r) & 3) (fp64), and the read groups of ds_read_b128 ({0-3,12-15,20-27}, ...) pair
+// every codeword c with four different rows -- conflict-free.  The alpha copy pre-rotates its
+// per-lane source addresses (the DMA's LDS side stays linear); beta publishes to rotated offsets.
+// A/B on one box: fp64 log-MAP 1180 -> 1211 Mbit/s, fp64 max-log 1900 -> 1928; fp32 lost 2 %
+// (1403 -> 1378, 2389 -> 2344), so fp32 keeps plain blocks.
+#ifndef TD_FOLD_SWZ
+#define TD_FOLD_SWZ 1   // 0: plain blocks, 1: rotated in fp64, 2: rotated in both precisions
+#endif
+template <typename T>
+constexpr bool kFoldSwz = TD_FOLD_SWZ == 2 || (TD_FOLD_SWZ == 1 && sizeof(T) == 8);
+template <typename T>
+constexpr int kBlkChunks = 8 * (int)sizeof(T) / 16;   // 16-B chunks per (row, codeword) block
+// element offset of state s (0..7) inside the block of row r
+template <typename T>
+__device__ __forceinline__ int blk_off(int s, int r)
+{
+    if (!kFoldSwz<T>) return s;
+    constexpr int E = 16 / (int)sizeof(T);   // states per chunk
+    return (((s / E) + r) & (kBlkChunks<T> - 1)) * E + (s & (E - 1));
+}
+// the 8 states of the block at blk (row r) in state order: one 16-B read per chunk
+template <typename T>
+__device__ __forceinline__ void load_block(const T* blk, int r, T (&v)[8])
+{
+    constexpr int E = 16 / (int)sizeof(T);
+    using V = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
+    if constexpr (kFoldSwz<T>) {
+#pragma unroll
+        for (int p = 0; p < kBlkChunks<T>; ++p) {
+            const V x = *reinterpret_cast<const V*>(blk + ((p + r) & (kBlkChunks<T> - 1)) * E);
+            __builtin_memcpy(&v[p * E], &x, 16);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = blk[j];
+    }
+}
+// row offset 8c + s (st_off) -> rotated
+template <typename T>
+__device__ __forceinline__ int rot_off(int off, int r)
+{
+    if (!kFoldSwz<T>) return off;
+    return (off & ~7) + blk_off<T>(off & 7, r);
+}
 
 // raw barrier: waits for this wave's LDS traffic only, so prefetched global loads stay in flight
 __device__ __forceinline__ void wg_sync_lds()
@@ -496,9 +547,17 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
 #pragma unroll
     for (int q = 0; q < n; ++q) {
-        // byte b of the copied block: log-MAP rows are the window's steps; max-log row r is step 3r
+        // LDS byte b of the copied block: row r = b / row_bytes (log-MAP rows are the window's
+        // steps; max-log row r is step ck_step(r)), chunk pc of codeword block cb, which holds the
+        // block's chunk (pc - r) mod kBlkChunks (blk_off)
         const int b = q * kDmaBytes + lane * 16;
-        const int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
+        int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
+        if constexpr (kFoldSwz<T>) {
+            const int r = b / row_bytes, w = b % row_bytes;
+            constexpr int blk = 8 * (int)sizeof(T);
+            const int pc = ((w % blk) / 16 - r) & (kBlkChunks<T> - 1);
+            off = (ALGO == 1 ? ck_step(r) : r) * row_bytes + (w / blk) * blk + pc * 16;
+        }
         dma16(lds + q * kDmaBytes, src + off);
     }
 }
@@ -702,7 +761,7 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
             if (kBetaBatch)
                 bs[k] = v;
             else
-                Bvw[k * kLanes + lc.st_off[(k + 1) % 3]] = v;
+                Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = v;
         };
         // operands read one step group ahead (the next group's inputs load under this group's chain)
         StepIn<T> b2 = beta_in<T, 2>(sm, tb, kW - 1, c, lc, tmw);
@@ -730,11 +789,11 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
         }
         if (kBetaBatch)
 #pragma unroll
-            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + lc.st_off[(k + 1) % 3]] = bs[k];
+            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
     } else {
         for (int k = n - 1; k >= 0; --k) {
             const int ph1 = (k + 1) % 3;   // constant indices only: a runtime index into lc moves it to scratch
-            Bvw[k * kLanes + (ph1 == 0 ? lc.st_off[0] : ph1 == 1 ? lc.st_off[1] : lc.st_off[2])] = beta;
+            Bvw[k * kLanes + rot_off<T>(ph1 == 0 ? lc.st_off[0] : ph1 == 1 ? lc.st_off[1] : lc.st_off[2], k)] = beta;
             beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, tmw);
         }
     }
@@ -784,23 +843,21 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
     T a[8], b[8], t0[8], t1[8];
     const T* bv = &sm.Bv[t & 1][k][c * 8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = bv[j];
+    load_block<T>(bv, k, b);
     if constexpr (ALGO == 1) {
         // alpha[.][i] from the last stored step ks <= k, recomputed through the steps in between
         // exactly as the alpha wave computed them (:975-1001)
         int ks;
-        const T* av = &sm.Av[t % kAvSlots][ck_row_of(k, ks)][c * 8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = av[j];
+        const int r = ck_row_of(k, ks);
+        const T* av = &sm.Av[t % kAvSlots][r][c * 8];
+        load_block<T>(av, r, a);
         for (int s = ks; s < k; ++s) {
             const T* gs = &sm.G[t % 3][s][c][0];
             alpha_recompute<T>(a, gs[0], gs[1]);
         }
     } else {
         const T* av = &sm.Av[t % kAvSlots][k][c * 8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = av[j];
+        load_block<T>(av, k, a);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
