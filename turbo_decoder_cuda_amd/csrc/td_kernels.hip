@@ -112,20 +112,29 @@ __device__ __forceinline__ int bucket_dev<float>(float d)
 // the clamped bit field and thr, vlo, vhi are ds_read offsets 0, 128, 384 B of it (one
 // ds_read2 + one ds_read, no address add on the chain).
 constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last bucket
-constexpr int kLutCols = 16;
-constexpr int kLutElems = 2 * kLutRows * kLutCols;
+// fp32: 32 columns.  Its 4-byte reads are served 32 lanes per LDS cycle on 32 banks, so with 16
+// columns lanes l and l+16 shared a bank whenever their buckets differed (SQ_LDS_BANK_CONFLICT
+// was 28 % of the fp32 kernel's LDS cycles).  fp64 keeps 16: 8-byte elements in 16 columns
+// already cover the 32 banks that ds_read2_b64 serves per cycle, and 32 would not fit in LDS.
+#ifndef TD_LUT32
+#define TD_LUT32 1
+#endif
+template <typename T>
+constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) ? 32 : 16;
+template <typename T>
+constexpr int kLutElems = 2 * kLutRows * kLutCols<T>;
 
 template <typename T>
 __device__ __forceinline__ const T* lut_origin(const T* col)
 {
-    return col - 2 * BucketBits<T>::base * kLutCols;
+    return col - 2 * BucketBits<T>::base * kLutCols<T>;
 }
 
 // fill a table copy: element e of the 2 * kLutRows * 16 (one thread per element)
 template <typename T>
 __device__ __forceinline__ T lut_elem(const LutEntry<T>* lut, int e)
 {
-    const int q = e / (2 * kLutCols), f = (e / kLutCols) & 1;
+    const int q = e / (2 * kLutCols<T>), f = (e / kLutCols<T>) & 1;
     if (q >= kLutSize) return f ? (T)lut[kLutSize - 1].vhi : (T)INFINITY;
     return f ? (T)lut[q].vlo : (T)lut[q].thr;
 }
@@ -136,12 +145,12 @@ struct LutRow {
 template <typename T>
 __device__ __forceinline__ LutRow lut_row(T d)
 {
-    return LutRow{bucket_dev<T>(d) * 2 * kLutCols};
+    return LutRow{bucket_dev<T>(d) * 2 * kLutCols<T>};
 }
 template <typename T>
 __device__ __forceinline__ T lut_pick(const T* lut, LutRow r, T d)
 {
-    const T thr = lut[r.o], lo = lut[r.o + kLutCols], hi = lut[r.o + 3 * kLutCols];
+    const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
     return fabs(d) >= thr ? hi : lo;
 }
 
@@ -242,7 +251,7 @@ constexpr int kTileDma = (kTileChunks<T> + kLanes - 1) / kLanes;   // DMA instru
 
 template <typename T>
 struct Smem {
-    T lut[kLutElems];   // max* table: [bucket][thr | v][16 columns] (see lut_origin)
+    T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
     T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
@@ -614,8 +623,8 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
         h.d = h.xp - h.xs;
         const LutRow r = lut_row(h.d);
         h.thr = lut[r.o];
-        h.lo = lut[r.o + kLutCols];
-        h.hi = lut[r.o + 3 * kLutCols];
+        h.lo = lut[r.o + kLutCols<T>];
+        h.hi = lut[r.o + 3 * kLutCols<T>];
     }
 #ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
     if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
@@ -664,8 +673,8 @@ __device__ __forceinline__ StepHalf<T> beta_issue(T beta, const StepIn<T>& in, c
         h.d = h.xp - h.xs;
         const LutRow r = lut_row(h.d);
         h.thr = lut[r.o];
-        h.lo = lut[r.o + kLutCols];
-        h.hi = lut[r.o + 3 * kLutCols];
+        h.lo = lut[r.o + kLutCols<T>];
+        h.hi = lut[r.o + 3 * kLutCols<T>];
     }
     return h;
 }
@@ -1064,13 +1073,13 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
 template <typename T>
 __device__ __forceinline__ void lut_to_lds(const DecodeParams<T>& p, Smem<T>& sm, int tid)
 {
-    for (int e = tid; e < kLutElems; e += kWaves * kLanes) sm.lut[e] = lut_elem<T>(p.lut, e);
+    for (int e = tid; e < kLutElems<T>; e += kWaves * kLanes) sm.lut[e] = lut_elem<T>(p.lut, e);
 }
 
 template <typename T>
 __device__ __forceinline__ const T* lut_col(const Smem<T>& sm, int lane)
 {
-    return lut_origin(sm.lut + (lane % kLutCols));
+    return lut_origin(sm.lut + (lane % kLutCols<T>));
 }
 
 template <typename T>
@@ -1378,13 +1387,13 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
 template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
-    __shared__ T lut_s[kLutElems];
+    __shared__ T lut_s[kLutElems<T>];
     if constexpr (ALGO == 0) {
-        for (int e = threadIdx.x; e < kLutElems; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
+        for (int e = threadIdx.x; e < kLutElems<T>; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const T* lut = lut_origin(lut_s + (lane % kLutCols));
+    const T* lut = lut_origin(lut_s + (lane % kLutCols<T>));
     // wave -> (decoder, sub-block, 64 codewords); everything but the codeword is wave-uniform
     const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const int cw_waves = a.Bp >> 6, per_dec = a.nS * cw_waves;
