@@ -965,8 +965,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         constexpr int kF = kTileDma<T>;
         auto fstep = [&](int t) {
             TD_STAMP(f0);
+#ifdef TD_DIAG_NOCONVERT   // diagnostics only (wrong results): the F pass without the loader's LDS
+            // traffic but for the last three windows, whose tiles (write positions) the B pass uses
+            if (t + 1 <= tl && t + 1 >= tl - 2) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
+            if (min(t + 3, tl) >= tl - 2) tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
+#else
             if (t + 1 <= tl) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
             tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
+#endif
             vm_wait<kF>();   // window t+2 has landed
             TD_STAMP(f1);
             wg_sync_lds();
