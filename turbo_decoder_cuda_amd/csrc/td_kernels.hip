@@ -303,6 +303,17 @@ __device__ __forceinline__ void load_block(const T* blk, int r, T (&v)[8])
         for (int j = 0; j < 8; ++j) v[j] = blk[j];
     }
 }
+// Rotation of alpha block (row r, codeword c).  Log-MAP: r (rows are the fold lanes' steps k).
+// Max-Log-MAP rows are checkpoints, r = k / 3, so the read groups hold up to three lanes of one
+// row; rotating by r + 2 (c >> 2) keeps their blocks' slots apart as well.
+#ifndef TD_MLAV_ROT
+#define TD_MLAV_ROT 1
+#endif
+template <int ALGO>
+__device__ __forceinline__ int av_rot(int r, int c)
+{
+    return (ALGO == 1 && TD_MLAV_ROT) ? r + 2 * (c >> 2) : r;
+}
 // row offset 8c + s (st_off) -> rotated
 template <typename T>
 __device__ __forceinline__ int rot_off(int off, int r)
@@ -558,13 +569,13 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     for (int q = 0; q < n; ++q) {
         // LDS byte b of the copied block: row r = b / row_bytes (log-MAP rows are the window's
         // steps; max-log row r is step ck_step(r)), chunk pc of codeword block cb, which holds the
-        // block's chunk (pc - r) mod kBlkChunks (blk_off)
+        // block's chunk (pc - av_rot) mod kBlkChunks (blk_off)
         const int b = q * kDmaBytes + lane * 16;
         int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
         if constexpr (kFoldSwz<T>) {
             const int r = b / row_bytes, w = b % row_bytes;
             constexpr int blk = 8 * (int)sizeof(T);
-            const int pc = ((w % blk) / 16 - r) & (kBlkChunks<T> - 1);
+            const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
             off = (ALGO == 1 ? ck_step(r) : r) * row_bytes + (w / blk) * blk + pc * 16;
         }
         dma16(lds + q * kDmaBytes, src + off);
@@ -859,7 +870,7 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
         int ks;
         const int r = ck_row_of(k, ks);
         const T* av = &sm.Av[t % kAvSlots][r][c * 8];
-        load_block<T>(av, r, a);
+        load_block<T>(av, av_rot<ALGO>(r, c), a);
         for (int s = ks; s < k; ++s) {
             const T* gs = &sm.G[t % 3][s][c][0];
             alpha_recompute<T>(a, gs[0], gs[1]);
