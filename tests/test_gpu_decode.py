@@ -50,6 +50,22 @@ def test_batch_vs_oracle_every_iteration(K, f1, f2, B, ebn0):
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
 
 
+# LTE sizes with their 36.212 Table 5.1.3-3 parameters: 5 to 171 windows of the kernel, every
+# residue of L = K+3 mod the 12-step window that LTE sizes take (3, 7, 11), ragged batches
+@pytest.mark.parametrize("K,f1,f2", [(48, 7, 12), (56, 19, 42), (120, 103, 90), (136, 9, 34),
+                                     (512, 31, 64), (2048, 31, 64)])
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+def test_lte_sizes_vs_oracle(K, f1, f2, algo):
+    B, iters = 11, 3
+    _, flow = O.synth_batch(K, f1, f2, 0.4, 900 + K, B)
+    bits, le = _decode_all(K, f1, f2, iters, flow, algo=algo)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(B):
+        ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
+        assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
+        assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+
+
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_maxlog_vs_oracle(precision):
     K, f1, f2, B, iters = 1024, 31, 64, 8, 4
