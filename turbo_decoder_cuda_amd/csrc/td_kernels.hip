@@ -763,10 +763,11 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
 #define TD_BETA_PIN 1
 #endif
 constexpr bool kBetaBatch = TD_BETA_BATCH != 0;   // beta published once per window, not per step
-// operand prefetch pinned behind a table read: fp64 only (A/B on one box, config 2: fp64
-// 1192 -> 1207 Mbit/s; fp32 log-MAP 1461 -> 1436, so fp32 keeps the compiler's placement)
-template <typename T>
-constexpr bool kBetaPin = TD_BETA_PIN != 0 && sizeof(T) == 8;
+// operand prefetch pinned behind a table read (A/B on one box, config 2: fp64 1192 -> 1207
+// Mbit/s).  fp32 log-MAP lost with it before its table went to 32 columns (1461 -> 1436) and gains
+// with it since (with beta at priority 2: 1414 -> 1443); fp32 Max-Log-MAP still loses (-0.4 %).
+template <typename T, int ALGO>
+constexpr bool kBetaPin = TD_BETA_PIN != 0 && (sizeof(T) == 8 || ALGO == 0);
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime)
 template <typename T, int ALGO>
@@ -793,11 +794,11 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
             put(k, beta);
             const StepHalf<T> h = beta_issue<T, ALGO, 2>(beta, b2, lut, lc);
             // the next group's operands, issued right behind this step's table read (TD_BETA_PIN)
-            if (kBetaPin<T>) __builtin_amdgcn_sched_barrier(0);
+            if (kBetaPin<T, ALGO>) __builtin_amdgcn_sched_barrier(0);
             const StepIn<T> n2 = beta_in<T, 2>(sm, tb, kn, c, lc, tmw);
             const StepIn<T> n1 = beta_in<T, 1>(sm, tb, kn - 1, c, lc, tmw);
             const StepIn<T> n0 = beta_in<T, 0>(sm, tb, kn - 2, c, lc, tmw);
-            if (kBetaPin<T>) __builtin_amdgcn_sched_barrier(0);
+            if (kBetaPin<T, ALGO>) __builtin_amdgcn_sched_barrier(0);
             beta = step_done<T, ALGO>(h) - b2.tm;   // :1019
             put(k - 1, beta);
             beta = beta_step<T, ALGO, 1>(beta, b1, lut, lc);
@@ -1113,7 +1114,7 @@ __device__ __forceinline__ Smem<T>* smem()
 #define TD_BETA_PRIO_F64 2
 #endif
 #ifndef TD_BETA_PRIO_F32
-#define TD_BETA_PRIO_F32 0   // fp32: the folds, not beta, bound the B pass (1430 -> 1451 Mbit/s)
+#define TD_BETA_PRIO_F32 2   // fp32 log-MAP: 0 measured best before its table went to 32 columns; now 2 (1414 -> 1436)
 #endif
 #ifndef TD_BETA_PRIO_MAXLOG
 #define TD_BETA_PRIO_MAXLOG 0
