@@ -167,6 +167,13 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     alg_bytes = bytes_cw * a.batch
     achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9 if turbo_ms > 0 else 0.0
     cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}" + (f"_w{a.window}g{a.overlap}" if a.window else "")
+    traffic = load_traffic(cfg_key)
+    # measured HBM bytes (PMC) per launch over the live kernel time: what the memory system
+    # actually moves (the exact kernel streams alpha / tempmax through HBM by design)
+    traffic_gbs = traffic / (turbo_ms * 1e-3) / 1e9 if (traffic and turbo_ms > 0) else None
+    # fp64 VALU work of the exact schedule (~133 ops per trellis step and SISO,
+    # max* counted as one op) over the live kernel time
+    valu_tops = a.batch * (a.K + 3) * 2 * a.iters * 133 / (turbo_ms * 1e-3) / 1e12 if turbo_ms > 0 else 0.0
     cfg_no = "5" if a.window else ("2" if a.algo == "logmap" else "3")
     return {
         "metric": METRIC,
@@ -198,7 +205,13 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6),
-            "traffic": load_traffic(cfg_key),
+            "traffic": traffic,
+            "traffic_gbs": round(traffic_gbs, 1) if traffic_gbs else None,
+            "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
+            "limiter": ("latency of the serial alpha / beta recursions (one dependent trellis step at a time "
+                        "per codeword; DESIGN.md 3.2): neither HBM nor VALU is saturated") if not a.window else
+                       "VALU / LDS issue of the sub-block chains (DESIGN.md 8.3)",
+            "valu_top_s": round(valu_tops, 3),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_codeword": bytes_cw,
             "kernel_ms_avg": round(turbo_ms, 4),

@@ -59,8 +59,10 @@ typedef struct td_handle td_handle;
 int td_create(td_handle** out, const td_params* p);
 /* Replaces TurboCodingRelease (log_map.cpp:1330-1345). */
 int td_destroy(td_handle* h);
-/* Size the device workspace for batches up to B codewords.  td_decode_device grows it on
- * demand; call td_reserve first when the decode is captured into a hipGraph. */
+/* Size the device workspace for batches up to B codewords (and, with a windowed schedule set by
+ * td_set_window, the windowed schedule's buffers).  td_decode_device grows them on demand, which
+ * synchronises the device; call td_reserve (after td_set_window) before a decode is captured
+ * into a hipGraph. */
 int td_reserve(td_handle* h, int B);
 
 /*
@@ -73,6 +75,10 @@ int td_reserve(td_handle* h, int B);
  *   d_le    nullable, [B][iterations][2][K+3] extrinsic Le after SISO1 and SISO2
  *           (:1234-1238, :1255-1259), same dtype as d_llr.
  *   stream  hipStream_t (NULL = default stream).  Asynchronous; no host synchronisation.
+ * A handle owns ONE device workspace: decodes on one handle never overlap.  A decode issued on a
+ * different stream than the previous one waits on the device (hipStreamWaitEvent) until the
+ * previous decode is done with the workspace; for concurrent decodes use one handle per stream.
+ * A handle is not thread-safe: one host thread uses it at a time.
  */
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                      void* stream);

@@ -187,3 +187,34 @@ def test_rand_window_jump_matches_glibc_stream():
                 x.append(v)
                 outs.append(v >> 1)
             assert outs == list(ref[d:d + 40])
+
+
+def test_compat_rejects_more_iterations_than_flow_decoded_rows(driver, tmp_path):
+    """main.cpp sizes flow_decoded as N_ITERATION (15) rows (main.cpp:153): TD_ITERATIONS above 15
+    would make TurboDecoding write past the caller's buffer, so TurboCodingInit refuses it
+    (exit 1, like the reference's init failures) before any device work."""
+    K = 40
+    np.zeros(3 * K + 12).tofile(tmp_path / "flow.bin")
+    for bad in ("16", "0"):
+        r = subprocess.run([driver, "decode", str(K), "3", "10", "1", str(tmp_path / "flow.bin"),
+                            str(tmp_path / "out.bin")], env={**os.environ, "TD_ITERATIONS": bad},
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 1 and "TD_ITERATIONS" in r.stdout, (bad, r.stdout, r.stderr)
+
+
+def test_decode_output_buffer_checks():
+    """TurboCodec.decode validates caller-supplied output buffers before the kernels write
+    B*iterations*K bits / B*iterations*2*(K+3) Le into them (dtype, shape, device, layout)."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    chk = TurboCodec._check_out
+    dev = torch.device("cpu")
+    chk("bits", torch.empty((4, 8), dtype=torch.uint8), torch.uint8, (4, 8), dev)
+    bad = [torch.empty((4, 8), dtype=torch.int32),          # dtype
+           torch.empty((4, 3, 8), dtype=torch.uint8),       # all_iters shape given to a final-only decode
+           torch.empty((8, 4), dtype=torch.uint8).t(),      # not contiguous
+           torch.empty((3, 8), dtype=torch.uint8)]          # too few rows
+    for t in bad:
+        with pytest.raises(ValueError):
+            chk("bits", t, torch.uint8, (4, 8), dev)

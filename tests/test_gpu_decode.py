@@ -164,3 +164,52 @@ def test_compat_turbo_decoding(driver, tmp_path, name):
     assert np.array_equal(out[:, :it].astype(np.uint8), d["bits"])
     flow2 = np.fromfile(str(tmp_path / "out.bin") + ".flow", dtype=np.float64).reshape(nf, -1)
     assert np.array_equal(flow2, d["flow"] * 0.5)
+
+
+def test_decode_rejects_bad_buffers():
+    """Shape / dtype / device checks of TurboCodec.decode (the kernels would write past a short
+    buffer): wrong stream length, all_iters bits of the final-only shape, Le of the other dtype."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, B, iters = 40, 4, 2
+    dev = _dev()
+    with TurboCodec(K, 3, 10, iterations=iters) as c:
+        good = torch.zeros((B, 3 * K + 12), dtype=torch.float64, device=dev)
+        with pytest.raises(ValueError):
+            c.decode(torch.zeros((B, 3 * K + 11), dtype=torch.float64, device=dev))
+        with pytest.raises(ValueError):
+            c.decode(good, torch.empty((B, K), dtype=torch.uint8, device=dev), all_iters=True)
+        with pytest.raises(ValueError):
+            c.decode(good, le=torch.empty((B, iters, 2, K + 3), dtype=torch.float32, device=dev))
+        with pytest.raises(ValueError):
+            c.decode(good, le=torch.empty((B, iters, 2, K + 2), dtype=torch.float64, device=dev))
+        c.decode(good, torch.empty((B, iters, K), dtype=torch.uint8, device=dev), all_iters=True,
+                 le=torch.empty((B, iters, 2, K + 3), dtype=torch.float64, device=dev))
+        torch.cuda.synchronize()
+
+
+def test_one_handle_two_streams():
+    """One handle, decodes issued alternately on two streams with no host synchronisation: the
+    handle orders them on its workspace (td_decode_device waits on the previous decode's event),
+    so every batch decodes to the oracle's bits."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2, B, iters = 1024, 31, 64, 16, 3
+    dev = _dev()
+    flows = [O.synth_batch(K, f1, f2, 0.3 + 0.1 * k, 300 + k, B)[1] for k in range(4)]
+    xs = [torch.from_numpy(f).to(dev) for f in flows]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    torch.cuda.synchronize()
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        outs = []
+        for k, x in enumerate(xs):
+            s = streams[k % 2]
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                outs.append(c.decode(x, stream=s))
+        torch.cuda.synchronize()
+    for f, b in zip(flows, outs):
+        ob = O.decode_batch(np.ascontiguousarray(f), K, f1, f2, iters, nthreads=4)
+        assert np.array_equal(b.cpu().numpy(), ob)

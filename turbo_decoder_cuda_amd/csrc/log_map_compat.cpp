@@ -86,7 +86,13 @@ void rsc(const int* u, int K, int* sys, int* par)
 
 void TurboCodingInit()
 {
+    // main.cpp sizes flow_decoded as N_ITERATION (15) rows of K (main.cpp:153) and TurboDecoding
+    // writes one row per iteration: more than 15 would write past the caller's buffer.
     g_iters = env_int("TD_ITERATIONS", 15);
+    if (g_iters < 1 || g_iters > 15) {
+        std::printf("turbo_mi355x: TD_ITERATIONS=%d is outside [1, 15] (N_ITERATION rows of flow_decoded)\n", g_iters);
+        std::exit(1);
+    }
     open_handle(source_length);
 }
 

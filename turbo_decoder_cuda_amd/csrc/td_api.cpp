@@ -74,6 +74,13 @@ struct td_handle {
     td::WindowParams wp{0, 0, 0, 0, 1.0f};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
+    // Workspace ordering across streams: every decode uses the same d_ws / d_wws, so a decode
+    // issued on a stream other than the previous decode's first waits (on the device) for that
+    // decode to finish with the workspace.  Decodes on one handle therefore never overlap; callers
+    // that want concurrent decodes use one handle per stream.
+    hipEvent_t ws_free = nullptr;   // recorded after the last decode's kernels
+    hipStream_t ws_stream = nullptr;
+    bool ws_pending = false;
 };
 
 namespace td {
@@ -190,14 +197,25 @@ int groups_for(int B)
 // the windowed schedule's buffers: the workspace's extrinsic pair plus a second pair (concurrent
 // schedule), the alpha checkpoints of each decoder and the NII metrics [2 parity][2 dec][B][nS][2][8],
 // grown on demand
-template <typename T>
-int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& wb)
+struct WinCarve {
+    size_t arrK, arrC, nii, total;
+};
+WinCarve win_carve(const td_handle* h, int B)
 {
-    const size_t arrK = align_up((size_t)dp.G * dp.K * 8 * sizeof(T), 256);
-    const size_t nii = (size_t)2 * 2 * dp.B * td::window_subblocks(dp.L, h->wp.window) * 16 * sizeof(T);
-    const size_t arrC =
-        align_up(td::window_ckpt_elems(dp.B, dp.L, h->wp.window, sizeof(T) == 4) * sizeof(T), 256);
-    const size_t need = 2 * arrK + 2 * arrC + nii;
+    const size_t elem = h->elem;
+    const int K = h->p.K, L = K + td::kMemory, G = groups_for(B);
+    WinCarve c{};
+    c.arrK = align_up((size_t)G * K * 8 * elem, 256);
+    c.nii = (size_t)2 * 2 * B * td::window_subblocks(L, h->wp.window) * 16 * elem;
+    c.arrC = align_up(td::window_ckpt_elems(B, L, h->wp.window, elem == 4) * elem, 256);
+    c.total = 2 * c.arrK + 2 * c.arrC + c.nii;
+    return c;
+}
+
+// grow the windowed-schedule buffers to `need` bytes (never inside a decode that is being
+// captured: td_reserve sizes them for the handle's window settings beforehand)
+int ensure_wws(td_handle* h, size_t need)
+{
     if (need > h->wws_bytes) {
         if (h->d_wws) {
             TD_HIP(hipDeviceSynchronize());
@@ -211,6 +229,16 @@ int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& 
         }
         h->wws_bytes = need;
     }
+    return TD_OK;
+}
+
+template <typename T>
+int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& wb)
+{
+    const WinCarve c = win_carve(h, dp.B);
+    const size_t arrK = c.arrK, arrC = c.arrC;
+    const int rc = ensure_wws(h, c.total);
+    if (rc) return rc;
     char* w = static_cast<char*>(h->d_wws);
     wb.ext12[0] = dp.ext12;
     wb.ext21[0] = dp.ext21;
@@ -254,6 +282,13 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.B = B;
     dp.iters = h->p.iterations;
     dp.all_iters = all_iters ? 1 : 0;
+    td::WindowBufs<T> wb{};
+    if (h->wp.window) {   // sized before anything is enqueued (a growth synchronises the device)
+        rc = window_bufs<T>(h, dp, wb);
+        if (rc) return rc;
+    }
+    if (!h->ws_free) TD_HIP(hipEventCreateWithFlags(&h->ws_free, hipEventDisableTiming));
+    if (h->ws_pending && st != h->ws_stream) TD_HIP(hipStreamWaitEvent(st, h->ws_free, 0));
     hipEvent_t* ev = nullptr;
     if (h->prof) {
         if (h->nev == h->ev.size()) {
@@ -261,22 +296,24 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
             for (auto& x : tri) TD_HIP(hipEventCreate(&x));
             h->ev.push_back(tri);
         }
-        ev = h->ev[h->nev++].data();
+        ev = h->ev[h->nev].data();   // claimed (nev advanced) only once all three are recorded
         TD_HIP(hipEventRecord(ev[0], st));
     }
     hipError_t e = td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
-    if (h->wp.window) {
-        td::WindowBufs<T> wb{};
-        rc = window_bufs<T>(h, dp, wb);
-        if (rc) return rc;
+    if (h->wp.window)
         e = td::launch_window<T>(dp, h->wp, wb, st);
-    } else {
+    else
         e = td::launch_turbo<T>(dp, st);
-    }
     if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
-    if (ev) TD_HIP(hipEventRecord(ev[2], st));
+    if (ev) {
+        TD_HIP(hipEventRecord(ev[2], st));
+        ++h->nev;
+    }
+    TD_HIP(hipEventRecord(h->ws_free, st));
+    h->ws_stream = st;
+    h->ws_pending = true;
     return TD_OK;
 }
 
@@ -543,6 +580,7 @@ int td_destroy(td_handle* h)
     if (h->d_wws) (void)hipFree(h->d_wws);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
+    if (h->ws_free) (void)hipEventDestroy(h->ws_free);
     delete h;
     return TD_OK;
 }
@@ -551,7 +589,9 @@ int td_reserve(td_handle* h, int B)
 {
     if (!h || B < 1) return fail(TD_EINVAL, "td_reserve: bad argument");
     TD_HIP(hipSetDevice(h->p.device));
-    return ensure_ws(h, groups_for(B));
+    const int rc = ensure_ws(h, groups_for(B));
+    if (rc || !h->wp.window) return rc;
+    return ensure_wws(h, win_carve(h, B).total);   // the windowed schedule's buffers as well
 }
 
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,

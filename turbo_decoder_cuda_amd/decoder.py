@@ -102,10 +102,18 @@ class TurboCodec:
         want = torch.float64 if self.precision == "f64" else torch.float32
         if llr.dtype != want or not llr.is_cuda or not llr.is_contiguous():
             raise ValueError(f"llr must be a contiguous {want} CUDA tensor")
+        if llr.ndim != 2 or llr.shape[1] != stream_length(self.K):
+            raise ValueError(f"llr must be [B, {stream_length(self.K)}] (3K+12), got {tuple(llr.shape)}")
+        if llr.device.index != self.device:
+            raise ValueError(f"llr is on {llr.device}, the codec on cuda:{self.device}")
         B = llr.shape[0]
+        shape = (B, self.iterations, self.K) if all_iters else (B, self.K)
         if bits is None:
-            shape = (B, self.iterations, self.K) if all_iters else (B, self.K)
             bits = torch.empty(shape, dtype=torch.uint8, device=llr.device)
+        else:
+            self._check_out("bits", bits, torch.uint8, shape, llr.device)
+        if le is not None:
+            self._check_out("le", le, want, (B, self.iterations, 2, self.L), llr.device)
         if stream is None:
             stream = torch.cuda.current_stream(llr.device)
         N.check(N.lib().td_decode_device(self._h, C.c_void_p(llr.data_ptr()), B, C.c_void_p(bits.data_ptr()),
@@ -113,8 +121,20 @@ class TurboCodec:
                                          C.c_void_p(stream.cuda_stream)))
         return bits
 
+    @staticmethod
+    def _check_out(name, t, dtype, shape, device) -> None:
+        """An output buffer the kernels write B*... elements into: its dtype, shape, device and
+        layout must be exactly what they assume, or they write past its end."""
+        if t.dtype != dtype or tuple(t.shape) != tuple(shape) or t.device != device or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)} on {device}, "
+                             f"got {t.dtype} {tuple(t.shape)} on {t.device}")
+
     def decode_raw(self, llr_ptr: int, B: int, bits_ptr: int, all_iters: bool = False, le_ptr: int = 0,
                    stream_ptr: int = 0) -> None:
+        """td_decode_device on raw device pointers (no checks possible here: the caller owns the
+        sizes -- llr B*(3K+12), bits B*K or B*iterations*K bytes, le B*iterations*2*(K+3))."""
+        if B < 0 or not llr_ptr or not bits_ptr:
+            raise ValueError("decode_raw: B >= 0 and non-null llr / bits pointers")
         N.check(N.lib().td_decode_device(self._h, C.c_void_p(llr_ptr), int(B), C.c_void_p(bits_ptr),
                                          int(all_iters), C.c_void_p(le_ptr) if le_ptr else None,
                                          C.c_void_p(stream_ptr) if stream_ptr else None))
