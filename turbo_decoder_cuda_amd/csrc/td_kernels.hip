@@ -699,6 +699,89 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
     return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), lut, lc);
 }
 
+// ------------------------------------------------------------------ scheduled windows (log-MAP)
+// A full window of either recursion as 12 unrolled steps with one fixed schedule per step:
+//   [chain up to the max* row address] [the row's three reads] [operand reads of a step two
+//   away] [HBM stores] [select + add]
+// as separate scheduling regions.  LDS returns a wave's reads in order, so any read issued
+// before the row read delays the chain by its LDS time.  Left to itself, the compiler sank the
+// next steps' operand reads in front of the row read, or split the row (ds_read2, operand reads,
+// then the row's third read), in every step group.  Reads issued right behind the row read
+// complete in its shadow, long before the next step's row read.
+#ifndef TD_SCHED
+#define TD_SCHED 1
+#endif
+
+template <typename T, int K>
+struct AlphaSched {
+    // alpha step K (phase K mod 3) of a full window: a = alpha_raw[.][i] in, alpha_raw[.][i+1] out;
+    // op[K % 3] holds this step's operands, op[(K + 2) % 3] receives step K+2's
+    static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
+                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0)
+    {
+        constexpr int PH = K % 3;
+        const StepIn<T> in = op[K % 3];
+        const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw (first level of the max)
+        T m = vmax(a, an);
+        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+        m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));   // tempmax[i] (:986-993)
+        const T alpha = a - m, ap = an - m;                   // :995-1000
+        const T xs = fma(lc.a_sg[PH], in.gs, alpha);
+        const T xp = fma(lc.a_pg[PH], in.gp, ap);
+        const T d = xp - xs;
+        const LutRow r = lut_row(d);
+        __builtin_amdgcn_sched_barrier(0);
+        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+        __builtin_amdgcn_sched_barrier(0);
+        gstore(ga + K * kLanes + lc.st_off[PH], alpha);
+        gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
+        __builtin_amdgcn_sched_barrier(0);
+        a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);
+        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0);
+    }
+};
+template <typename T>
+struct AlphaSched<T, kW> {
+    static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
+                                               const LaneConst<T>&, T*, T*, T*)
+    {
+    }
+};
+
+template <typename T, int K>
+struct BetaSched {
+    // beta step K (phase K mod 3, steps run K = kW-1 .. 0): beta[.][i+1] in, beta[.][i] out;
+    // bs[K] keeps the incoming beta for the window's publish; op[(K + 1) % 3] receives step K-2's
+    static __device__ __forceinline__ void run(T& beta, StepIn<T> (&op)[3], T (&bs)[kW], const Smem<T>& sm, int tb,
+                                               const T* lut, int c, const LaneConst<T>& lc, const T* tmw)
+    {
+        constexpr int PH = K % 3;
+        const StepIn<T> in = op[K % 3];
+        bs[K] = beta;
+        const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
+        const T xs = fma(lc.b_sg[PH], in.gs, beta);
+        const T xp = fma(lc.b_pg[PH], in.gp, bp);
+        const T d = xp - xs;
+        const LutRow r = lut_row(d);
+        __builtin_amdgcn_sched_barrier(0);
+        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K >= 2) op[(K + 1) % 3] = beta_in<T, (K - 2) % 3>(sm, tb, K - 2, c, lc, tmw);
+        __builtin_amdgcn_sched_barrier(0);
+        beta = (vmax(xs, xp) + (fabs(d) >= thr ? hi : lo)) - in.tm;   // :1012-1019
+        BetaSched<T, K - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw);
+    }
+};
+template <typename T>
+struct BetaSched<T, -1> {
+    static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], T (&)[kW], const Smem<T>&, int, const T*, int,
+                                               const LaneConst<T>&, const T*)
+    {
+    }
+};
+
 // alpha over the n steps of window t (window starts are = 0 mod 3); ga / gtm point at step t*kW.
 // Step k stores tempmax[i] at scratch index i - 1 (the B pass reads tempmax[i+1] at index i); at
 // t = 0 the first store (tempmax[0]) lands on index 0, which step 1 then overwrites.  The caller
@@ -708,6 +791,17 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
                                           const LaneConst<T>& lc, T* ga, T* gtm)
 {
     const int tb = t % 3;
+#if TD_SCHED
+    if constexpr (ALGO == 0) {
+        if (n == kW) {
+            StepIn<T> op[3];
+            op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
+            op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
+            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0));
+            return a;
+        }
+    }
+#endif
     T* pa0 = ga + lc.st_off[0];
     T* pa1 = ga + kLanes + lc.st_off[1];
     T* pa2 = ga + 2 * kLanes + lc.st_off[2];
@@ -776,6 +870,18 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
     const int tb = t % 3, xb = t & 1;
     T* Bvw = &sm.Bv[xb][0][0];
     const T* tmw = &sm.tm[xb][0][0];
+#if TD_SCHED
+    if (ALGO == 0 && n == kW) {
+        T bs[kW];   // beta[.][i+1] of step k, published after the window
+        StepIn<T> op[3];
+        op[(kW - 1) % 3] = beta_in<T, (kW - 1) % 3>(sm, tb, kW - 1, c, lc, tmw);
+        op[(kW - 2) % 3] = beta_in<T, (kW - 2) % 3>(sm, tb, kW - 2, c, lc, tmw);
+        BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw);
+#pragma unroll
+        for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
+        return beta;
+    }
+#endif
     if (n == kW) {
         T bs[kW];   // beta[.][i+1] of step k, stored by lane after the window (TD_BETA_BATCH)
         auto put = [&](int k, T v) {
