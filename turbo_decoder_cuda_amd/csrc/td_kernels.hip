@@ -699,6 +699,25 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
     return beta_step<T, ALGO, 2>(beta, beta_in<T, 2>(sm, tb, k, c, lc, tmw), lut, lc);
 }
 
+// Diagnostic build (TD_STAMPS) only: shader-clock reads around the 12 chain steps of a scheduled
+// window, summed into the wave's stamp slot 4 (the recursion's chain alone, without the window's
+// operand prologue, publish and barrier).
+#ifdef TD_STAMPS
+#define TD_CHAIN_T0(v)                              \
+    __builtin_amdgcn_sched_barrier(0);              \
+    const unsigned long long v = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0)
+#define TD_CHAIN_ACC(v)                                                       \
+    do {                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+        if (chain_st) *chain_st += __builtin_amdgcn_s_memtime() - (v);        \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+    } while (0)
+#else
+#define TD_CHAIN_T0(v)
+#define TD_CHAIN_ACC(v)
+#endif
+
 // ------------------------------------------------------------------ scheduled windows (log-MAP)
 // A full window of either recursion as 12 unrolled steps with one fixed schedule per step:
 //   [chain up to the max* row address] [the row's three reads] [operand reads of a step two
@@ -750,12 +769,19 @@ struct AlphaSched<T, kW> {
     }
 };
 
+// TD_BETA_SHADOW: each beta step writes its incoming beta[.][i+1] (the fold input of step i) into
+// the window's Bv rows behind its own row read, instead of the 12 writes (and their rotated
+// addresses) after the window, which the chain waited for at the window's barrier.
+#ifndef TD_BETA_SHADOW
+#define TD_BETA_SHADOW 1
+#endif
+
 template <typename T, int K>
 struct BetaSched {
     // beta step K (phase K mod 3, steps run K = kW-1 .. 0): beta[.][i+1] in, beta[.][i] out;
     // bs[K] keeps the incoming beta for the window's publish; op[(K + 1) % 3] receives step K-2's
     static __device__ __forceinline__ void run(T& beta, StepIn<T> (&op)[3], T (&bs)[kW], const Smem<T>& sm, int tb,
-                                               const T* lut, int c, const LaneConst<T>& lc, const T* tmw)
+                                               const T* lut, int c, const LaneConst<T>& lc, const T* tmw, T* Bvw)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -770,14 +796,16 @@ struct BetaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K >= 2) op[(K + 1) % 3] = beta_in<T, (K - 2) % 3>(sm, tb, K - 2, c, lc, tmw);
         __builtin_amdgcn_sched_barrier(0);
+        if (TD_BETA_SHADOW) Bvw[K * kLanes + rot_off<T>(lc.st_off[(K + 1) % 3], K)] = bs[K];
+        __builtin_amdgcn_sched_barrier(0);
         beta = (vmax(xs, xp) + (fabs(d) >= thr ? hi : lo)) - in.tm;   // :1012-1019
-        BetaSched<T, K - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw);
+        BetaSched<T, K - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
     }
 };
 template <typename T>
 struct BetaSched<T, -1> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], T (&)[kW], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, const T*)
+                                               const LaneConst<T>&, const T*, T*)
     {
     }
 };
@@ -788,8 +816,10 @@ struct BetaSched<T, -1> {
 // stores tempmax[L] after the last window.
 template <typename T, int ALGO>
 __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, const T* lut, int c,
-                                          const LaneConst<T>& lc, T* ga, T* gtm)
+                                          const LaneConst<T>& lc, T* ga, T* gtm,
+                                          unsigned long long* chain_st = nullptr)
 {
+    (void)chain_st;
     const int tb = t % 3;
 #if TD_SCHED
     if constexpr (ALGO == 0) {
@@ -797,7 +827,9 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
             StepIn<T> op[3];
             op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
             op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
+            TD_CHAIN_T0(c0);
             AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0));
+            TD_CHAIN_ACC(c0);
             return a;
         }
     }
@@ -865,8 +897,10 @@ constexpr bool kBetaPin = TD_BETA_PIN != 0 && (sizeof(T) == 8 || ALGO == 0);
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime)
 template <typename T, int ALGO>
-__device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, const T* lut, int c, const LaneConst<T>& lc)
+__device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, const T* lut, int c, const LaneConst<T>& lc,
+                                         unsigned long long* chain_st = nullptr)
 {
+    (void)chain_st;
     const int tb = t % 3, xb = t & 1;
     T* Bvw = &sm.Bv[xb][0][0];
     const T* tmw = &sm.tm[xb][0][0];
@@ -876,9 +910,12 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
         StepIn<T> op[3];
         op[(kW - 1) % 3] = beta_in<T, (kW - 1) % 3>(sm, tb, kW - 1, c, lc, tmw);
         op[(kW - 2) % 3] = beta_in<T, (kW - 2) % 3>(sm, tb, kW - 2, c, lc, tmw);
-        BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw);
+        TD_CHAIN_T0(c0);
+        BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
+        TD_CHAIN_ACC(c0);
+        if (!TD_BETA_SHADOW)
 #pragma unroll
-        for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
+            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
         return beta;
     }
 #endif
@@ -1062,7 +1099,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw);
+                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
@@ -1168,7 +1205,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = 0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wb = tl - j + 1;
-            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc);
+            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc,
+                                                                        st ? st + 4 : nullptr);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
