@@ -31,7 +31,8 @@ torch.cuda.synchronize()
 c.profile(True)
 bits = c.decode(x)
 _, kms, _ = c.kernel_ms()
-s = st.cpu().numpy().reshape(G, 4, 7).astype(np.float64)
+NS = slots // 4
+s = st.cpu().numpy().reshape(G, 4, NS).astype(np.float64)
 L = K + 3
 steps = 2 * iters * L
 print(f"B={B} {prec} {algo} kernel_ms={kms:.3f} errs={int((bits.cpu().numpy() != u).sum())}")
@@ -40,7 +41,15 @@ for w in range(4):
     fw, fwait, bw, bwait = (s[:, w, i].mean() / steps for i in range(4))
     print(f"  {roles[w]:14s} per SISO-step: F work {fw:7.1f}  F wait {fwait:7.1f}  B work {bw:7.1f}  B wait {bwait:7.1f}"
           f"  (slot4 {s[:, w, 4].mean() / steps:6.1f})")
-hw = st.cpu().numpy().reshape(G, 4, 7)[:, :, 6].astype(np.int64)
+kc, kr = s[:, :, 7], s[:, :, 8]
+clk = kc.sum() / kr.sum() * 0.1   # GHz (realtime ticks at 100 MHz)
+acc = s[:, :, 0:4].sum(axis=2)
+print(f"  clock {clk:.3f} GHz; kernel {kc.mean() / steps:.1f} cycles per SISO-step, of which the pass stamps cover "
+      f"{acc.mean() / steps:.1f} (unstamped: SISO prologues / epilogues, {(kc.mean() - acc.mean()) / steps:.1f})")
+for w in range(4):
+    print(f"  {roles[w]:14s} per SISO-step: SISO calls {s[:, w, 9].mean() / steps:7.1f}  SISO-end barrier "
+          f"{s[:, w, 10].mean() / steps:6.1f}  in-SISO unstamped {(s[:, w, 9] - s[:, w, 0:4].sum(axis=1)).mean() / steps:6.1f}")
+hw = st.cpu().numpy().reshape(G, 4, NS)[:, :, 6].astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15
 se = (hw >> 13) & 7
@@ -49,7 +58,7 @@ print("  waves of a group on distinct SIMDs: " + ", ".join(f"{k}:{int((distinct 
 same = lambda a, b: int((simd[:, a] == simd[:, b]).sum())
 print(f"  A/B share SIMD in {same(0, 1)} groups, A/F0 {same(0, 2)}, A/F1 {same(0, 3)}, B/F0 {same(1, 2)}, B/F1 {same(1, 3)}")
 # workgroups resident on the same CU (XCC, SE, SH, CU): which roles of the two share a SIMD
-xcc = st.cpu().numpy().reshape(G, 4, 7)[:, 0, 5].astype(np.int64) & 0xF
+xcc = st.cpu().numpy().reshape(G, 4, NS)[:, 0, 5].astype(np.int64) & 0xF
 sh = (hw >> 12) & 1
 key = [(int(xcc[g]), int(se[g, 0]), int(sh[g, 0]), int(cu[g, 0])) for g in range(G)]
 from collections import Counter, defaultdict  # noqa: E402

@@ -1,7 +1,8 @@
 // ubench_alpha.hip -- cycles per alpha step of the turbo decoder's forward recursion on gfx950,
 // one chain per wave (64 workgroups of one wave), operands in registers, max* table in LDS.
 // Variants: 0 table read after the group max (committed order), 1 speculative table read with the
-// bucket check, 2 speculative read without the check (timing only), 3 Max-Log-MAP.
+// bucket check, 2 speculative read without the check (timing only), 3 Max-Log-MAP, 4/5 folded
+// offsets (5 speculative row), 6 whole correction speculated (row and threshold side) + flag.
 // hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-honor-nans -fno-slp-vectorize -o scripts/ubench_alpha scripts/ubench_alpha.hip
 #include <hip/hip_runtime.h>
 
@@ -69,6 +70,37 @@ __device__ __forceinline__ double step2(double x, double sg, double gs, double p
     return fabs(d) >= t ? rh : rl;
 }
 
+// V 6: the whole max* correction speculated from the unnormalised difference (row AND threshold
+// compare), so the chain after the group max is sub, fma, max, add; the exact difference is only
+// checked (same bucket, same side of the row's threshold), OR-ed into a flag read per window.
+template <int V, int C0, int C1, int C2>
+__device__ __forceinline__ double step3(double x, double sg, double gs, double pg, double gp, const char* rowb, double* st,
+                                        unsigned& flag)
+{
+    const double an = dpp<C0>(x);
+    const double du = fma(pg, gp, an) - fma(sg, gs, x);
+    const int qu = bucket_raw(du);
+    const char* r = rowb + qu * 128;
+    const double t = *(const double*)r, l = *(const double*)(r + 64 * 128), h = *(const double*)(r + 65 * 128);
+    __builtin_amdgcn_sched_barrier(0);
+    double m = fmax(x, an);
+    m = fmax(m, dpp<C1>(m));
+    m = fmax(m, dpp<C2>(m));
+    const double al = x - m, ap = an - m;
+    if (st) {
+        asm volatile("global_store_dwordx2 %0, %1, off" :: "v"(st), "v"(al) : "memory");
+        asm volatile("global_store_dwordx2 %0, %1, off offset:8" :: "v"(st), "v"(m) : "memory");
+    }
+    const double xs = fma(sg, gs, al), xp = fma(pg, gp, ap);
+    if (V == 7) __builtin_amdgcn_sched_barrier(0);
+    const double mx = fmax(xs, xp);
+    const bool su = fabs(du) >= t;
+    const double f = su ? h : l;
+    const double d = xp - xs;
+    flag |= (unsigned)(bucket_raw(d) ^ qu) | (unsigned)((fabs(d) >= t) != su);
+    return mx + f;
+}
+
 template <int V, int C0, int C1, int C2>
 __device__ __forceinline__ double step(double x, double sg, double gs, double pg, double gp, const double* lut, double* st)
 {
@@ -117,7 +149,16 @@ __global__ void k(double* out, unsigned long long* cyc)
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     unsigned flag = 0;
     const char* rowb = (const char*)lut - 8152 * 128;
-    if (V >= 4) {
+    if (V >= 6) {
+        for (int i = 0; i < N; i += 3) {
+            x = step3<V, 0xB1, 0x4E, 0x141>(x, sg, gs, pg, gp, rowb, st, flag);
+            if (STORE) st += 64 * 64 * 2;
+            x = step3<V, 0x4E, 0x141, 0xB1>(x, -sg, gp, pg, gs, rowb, st, flag);
+            if (STORE) st += 64 * 64 * 2;
+            x = step3<V, 0x141, 0xB1, 0x4E>(x, sg, gp, -pg, gs, rowb, st, flag);
+            if (STORE) st += 64 * 64 * 2;
+        }
+    } else if (V >= 4) {
         for (int i = 0; i < N; i += 3) {
             x = step2<V, 0xB1, 0x4E, 0x141>(x, sg, gs, pg, gp, rowb, st, flag);
             if (STORE) st += 64 * 64 * 2;
@@ -171,5 +212,9 @@ int main()
     run<5, 0>("speculative, flag check, folded", out, cyc);
     run<4, 1>("after max folded + stores", out, cyc);
     run<5, 1>("speculative flag folded + stores", out, cyc);
+    run<6, 0>("full max* speculation, flag check", out, cyc);
+    run<6, 1>("full max* speculation + stores", out, cyc);
+    run<7, 0>("full speculation, select after the fmas", out, cyc);
+    run<7, 1>("full speculation, select after + stores", out, cyc);
     return 0;
 }

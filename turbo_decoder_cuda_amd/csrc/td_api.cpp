@@ -518,7 +518,8 @@ int td_create(td_handle** out, const td_params* p)
         td::LutEntry<float> l32[td::kLutSize];
         td::build_lut<double>(l64);
         td::build_lut<float>(l32);
-        if (!td::lut_vhi_is_next_vlo(l64) || !td::lut_vhi_is_next_vlo(l32)) {
+        if (!td::lut_vhi_is_next_vlo(l64) || !td::lut_vhi_is_next_vlo(l32) ||
+            !td::lut_one_threshold_per_bucket<double>() || !td::lut_one_threshold_per_bucket<float>()) {
             delete h;
             return fail(TD_EINVAL, "td_create: max* table does not have the chained form the kernels read");
         }
@@ -659,7 +660,7 @@ int td_debug_set_stamps(td_handle* h, void* d_buf)
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
-    return 4 * 7;   // [wave][slot]
+    return 4 * 11;   // [wave][slot] (td_kernels.hip kStampSlots)
 #else
     return 0;
 #endif

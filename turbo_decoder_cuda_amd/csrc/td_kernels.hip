@@ -85,7 +85,7 @@ __device__ __forceinline__ T group_max8(T v)
 
 // ------------------------------------------------------------------ max*
 // Exact bucket form of E_algorithm (td_tables.h, build_lut): the bucket index is a bit field of
-// d (exponent + 3 mantissa bits; the sign bit is outside the field, so d need not be |d|).
+// d (exponent + 2 mantissa bits; the sign bit is outside the field, so d need not be |d|).
 template <typename T>
 __device__ __forceinline__ int bucket_dev(T d);
 template <>
@@ -731,6 +731,26 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
 #define TD_SCHED 1
 #endif
 
+// max(xs, xp) + (|d| >= thr ? hi : lo), the max* of a scheduled step.  TD_ADDSEL forms both candidate
+// sums once the row lands and selects between them (one dependent fp64 op less on the chain, one
+// VALU more); the sums are pinned in registers so the compiler cannot fold them back into one add.
+#ifndef TD_ADDSEL
+#define TD_ADDSEL 0
+#endif
+template <typename T>
+__device__ __forceinline__ T sched_finish(T xs, T xp, T d, T thr, T lo, T hi)
+{
+    const T mx = vmax(xs, xp);
+    if constexpr (TD_ADDSEL != 0) {
+        T rl = mx + lo, rh = mx + hi;
+        touch(rl);
+        touch(rh);
+        return fabs(d) >= thr ? rh : rl;
+    } else {
+        return mx + (fabs(d) >= thr ? hi : lo);
+    }
+}
+
 template <typename T, int K>
 struct AlphaSched {
     // alpha step K (phase K mod 3) of a full window: a = alpha_raw[.][i] in, alpha_raw[.][i+1] out;
@@ -757,7 +777,7 @@ struct AlphaSched {
         gstore(ga + K * kLanes + lc.st_off[PH], alpha);
         gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
         __builtin_amdgcn_sched_barrier(0);
-        a = vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);
+        a = sched_finish(xs, xp, d, thr, lo, hi);
         AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0);
     }
 };
@@ -798,7 +818,7 @@ struct BetaSched {
         __builtin_amdgcn_sched_barrier(0);
         if (TD_BETA_SHADOW) Bvw[K * kLanes + rot_off<T>(lc.st_off[(K + 1) % 3], K)] = bs[K];
         __builtin_amdgcn_sched_barrier(0);
-        beta = (vmax(xs, xp) + (fabs(d) >= thr ? hi : lo)) - in.tm;   // :1012-1019
+        beta = sched_finish(xs, xp, d, thr, lo, hi) - in.tm;   // :1012-1019
         BetaSched<T, K - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
     }
 };
@@ -1067,7 +1087,9 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
 #define TD_STAMP(v)
 #define TD_ACC(slot, a, b)
 #endif
-constexpr int kStampSlots = 7;   // per wave: F pass, F wait, B work, B wait, -, -, HW_ID (see diag)
+constexpr int kStampSlots = 11;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
+                                 // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
+                                 // barriers (see diag)
 
 // The loader wave keeps one register set per stream, issued one iteration ahead and consumed
 // (stored to LDS) at the start of the next iteration before it is re-issued; it issues the same
@@ -1076,7 +1098,7 @@ constexpr int kStampSlots = 7;   // per wave: F pass, F wait, B work, B wait, -,
 
 // One SISO over the workgroup's 8 codewords.  Each role runs its own loops (so only that role's
 // state is live in its code); every role executes the same sequence of wg_sync_lds barriers:
-// 1 (F prologue) + nT (F iterations) + nT + 2 (B iterations).
+// 1 (F prologue) + nT (F iterations) + nB (B iterations).
 template <typename T, int ALGO>
 __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& dst, const Geom& gm, T* astore,
                         T* tmstore, const LaneTables* lt, int wave, int lane, unsigned long long* st)
@@ -1096,10 +1118,21 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         T a = lc.a_init0 ? (T)0 : (T)-kInfty;   // alpha[.][0] (:943,948), its tempmax is 0
         __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
+#ifdef TD_DIAG_FPAIR   // diagnostics only (wrong results): two alpha windows per F-pass barrier (on one tile)
+        for (int t = 0; t < nT; t += 2) {
+            TD_STAMP(f0);
+            a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
+                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
+            if (t + 1 < nT)
+                a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
+                                          ga0 + (size_t)(t + 1) * kW * kLanes, gtm0 + (size_t)(t + 1) * kW * kCw,
+                                          st ? st + 4 : nullptr);
+#else
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
                                       ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
+#endif
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
@@ -1142,7 +1175,11 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         tile_dma(sm, 2, src, dst, gm, min(2, tl), lane);
         vm_wait<kF>();
         wg_sync_lds();
+#ifdef TD_DIAG_FPAIR
+        for (int t = 0; t < nT; t += 2) fstep(t);
+#else
         for (int t = 0; t < nT; ++t) fstep(t);
+#endif
         // B pass iteration j (wa = tl - j) converts the tiles of wa (tiles tl-2..tl never left the
         // ring) and tempmax of wa (beta, next iteration) from staging slot j % 3 into the LDS slots
         // nobody reads this iteration, stages the same streams three windows lower into the slot it
@@ -1185,7 +1222,11 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         return;
     } else {
         wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
+#ifdef TD_DIAG_FPAIR
+        for (int t = 0; t < nT; t += 2) {
+#else
         for (int t = 0; t < nT; ++t) {
+#endif
             TD_STAMP(f0);
             TD_STAMP(f1);
             wg_sync_lds();
@@ -1367,6 +1408,9 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
 
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     unsigned long long st[kStampSlots] = {};
+#ifdef TD_STAMPS
+    const unsigned long long k_cyc0 = __builtin_amdgcn_s_memtime(), k_rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // SISO pass s = 2*it + dec
     for (int s = 0; s < 2 * p.iters; ++s) {
         const int it = s >> 1, dec = s & 1;
@@ -1381,12 +1425,19 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
         SisoDst<T> dst{dec ? p.ext21 : p.ext12, dec ? 2 : 3, p.K, nullptr, p.le_dump,
                        want_bits ? p.bits : nullptr, p.all_iters ? it : 0, p.all_iters ? p.iters * p.K : p.K,
                        s, p.iters * 2 * p.L};
+        TD_STAMP(s0);
         siso_wg<T, ALGO>(sm, src, dst, gm, p.astore, p.tmstore, p.lane, wave, lane, st);
+        TD_STAMP(s1);
         __syncthreads();   // extrinsic stores of this SISO visible to the next one's loads
+        TD_STAMP(s2);
+        TD_ACC(9, s0, s1);
+        TD_ACC(10, s1, s2);
     }
 #ifdef TD_STAMPS
     st[6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
     st[5] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    st[7] = __builtin_amdgcn_s_memtime() - k_cyc0;
+    st[8] = __builtin_amdgcn_s_memrealtime() - k_rt0;
     if (p.stamps && lane == 0)
         for (int q = 0; q < kStampSlots; ++q)
             p.stamps[((size_t)w.g * kWaves + wave) * kStampSlots + q] = st[q];

@@ -116,24 +116,26 @@ inline void build_qpp(int K, int f1, int f2, int* pi)
 }
 
 // Bucket geometry of the max* table.  The bucket index comes straight from the bits of
-// d = |y - x|: exponent + top 3 mantissa bits (8 buckets per octave), clamped to [0, 56]:
-//   bucket 0      d < 2^-4 * 1.125 (below the first threshold 0.08824)
-//   buckets 1..55 [2^e (1 + m/8), 2^e (1 + (m+1)/8)),  e = -4..2
-//   bucket 56     d >= 8                                 (f = 0)
-// Every bucket holds at most one threshold (relative threshold gaps >= 1.19 > 1 + 1/8), so
+// d = |y - x|: exponent + top 2 mantissa bits (4 buckets per octave), clamped to [0, 28]:
+//   bucket 0      d < 2^-4 * 1.25 (below the first threshold 0.08824)
+//   buckets 1..27 [2^e (1 + m/4), 2^e (1 + (m+1)/4)),  e = -4..2
+//   bucket 28     d >= 8                                 (f = 0)
+// Every bucket holds at most one threshold (checked by lut_one_threshold_per_bucket at td_create;
+// the closest pairs are 1.0502 | 1.2587 | 1.5078 | 1.8212 in [1, 2), one per quarter octave), so
 //   f(d) = (d >= thr[q]) ? vhi[q] : vlo[q]
-// reproduces the reference's linear scan (log_map.cpp:779-801) for every d >= 0.
-constexpr int kLutSize = 57;
+// reproduces the reference's linear scan (log_map.cpp:779-801) for every d >= 0.  (Three mantissa
+// bits, 57 buckets, give the same results with a table twice the size in LDS.)
+constexpr int kLutSize = 29;
 
 template <typename T>
 struct BucketBits;
 template <>
-struct BucketBits<double> {   // bits 17..30 of the high dword: 11 exponent + 3 mantissa bits
-    static constexpr int shift = 17, width = 14, base = (1023 - 4) << 3;
+struct BucketBits<double> {   // bits 18..30 of the high dword: 11 exponent + 2 mantissa bits
+    static constexpr int shift = 18, width = 13, base = (1023 - 4) << 2;
 };
 template <>
-struct BucketBits<float> {    // bits 20..30: 8 exponent + 3 mantissa bits
-    static constexpr int shift = 20, width = 11, base = (127 - 4) << 3;
+struct BucketBits<float> {    // bits 21..30: 8 exponent + 2 mantissa bits
+    static constexpr int shift = 21, width = 10, base = (127 - 4) << 2;
 };
 
 inline int bucket_of_bits(unsigned hi, int shift, int width, int base)
@@ -179,6 +181,18 @@ inline void build_lut(LutEntry<T>* lut)
         lut[q].vhi = val[base + 1 <= 15 ? base + 1 : 15];
         lut[q].pad = (T)0;
     }
+}
+
+// No bucket holds two thresholds (build_lut would keep only the last one).
+template <typename T>
+inline bool lut_one_threshold_per_bucket()
+{
+    using BB = BucketBits<T>;
+    int n[kLutSize] = {};
+    for (int k = 1; k < 16; ++k) ++n[bucket_of_bits(high_word((T)kIdx[k]), BB::shift, BB::width, BB::base)];
+    for (int q = 0; q < kLutSize; ++q)
+        if (n[q] > 1) return false;
+    return true;
 }
 
 // The device keeps only thr and vlo per bucket and reads vhi[q] as vlo[q+1] (the value just past
