@@ -144,6 +144,23 @@ __global__ void k(double* out, double a, unsigned long long* cyc, int mode)
                 }
             }
             break;
+        case 17:  // issue cost: 8 independent v_add_f64 chains (cycles per 8 adds)
+        case 18:  // issue cost: 8 independent v_add_u32 chains (cycles per 8 adds)
+            {
+                double v[8];
+                unsigned w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { v[j] = x * (j + 1); w[j] = threadIdx.x * (j + 3); }
+                for (int i = 0; i < N; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (mode == 17) v[j] = v[j] + a; else w[j] = w[j] + (unsigned)i;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x += v[j] + (double)w[j];
+            }
+            break;
         case 8:   // v_add_f64 pairs interleaved (2 independent chains)
             {
                 double y = x * 0.5;
@@ -170,8 +187,9 @@ int main()
                            "v_add_f32", "gmax3(dpp+max)+add", "int bfe+med3+lshl", "2x add_f64 interleaved",
                            "alpha step maxlog (regs)", "alpha step maxlog (lds g)", "ds_bpermute x2 lookup+add",
                            "3x ds_read_b64 + sel + add", "bfe+med3+cvt+add",
-                           "alpha logmap (table after max)", "alpha logmap (speculative table)", "alpha logmap spec + 2 stores"};
-    for (int mode = 0; mode < 17; ++mode) {
+                           "alpha logmap (table after max)", "alpha logmap (speculative table)", "alpha logmap spec + 2 stores",
+                           "8 indep v_add_f64 (per 8)", "8 indep v_add_u32 (per 8)"};
+    for (int mode = 0; mode < 19; ++mode) {
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);
         hipDeviceSynchronize();
         hipLaunchKernelGGL(k, dim3(64), dim3(64), 0, 0, out, 1.0000001, cyc, mode);

@@ -119,8 +119,11 @@ constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last buc
 #ifndef TD_LUT32
 #define TD_LUT32 1
 #endif
+#ifndef TD_LUT32_F64
+#define TD_LUT32_F64 0   // fp64 table in 32 columns (fits since the table went to 29 buckets)
+#endif
 template <typename T>
-constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) ? 32 : 16;
+constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) || (TD_LUT32_F64 && sizeof(T) == 8) ? 32 : 16;
 template <typename T>
 constexpr int kLutElems = 2 * kLutRows * kLutCols<T>;
 
@@ -405,6 +408,19 @@ __device__ __forceinline__ void gstore(double* p, double v)
 __device__ __forceinline__ void gstore(float* p, float v)
 {
     asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+// the same with a wave-uniform base in SGPRs, a per-lane 32-bit byte offset and an immediate (the
+// scheduled alpha windows: no per-step 64-bit address arithmetic)
+template <int IMM>
+__device__ __forceinline__ void gstore_s(double* base, unsigned voff, double v)
+{
+    asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
+}
+template <int IMM>
+__device__ __forceinline__ void gstore_s(float* base, unsigned voff, float v)
+{
+    asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
 }
 
 __device__ __forceinline__ unsigned lds_addr(const void* p)
@@ -789,6 +805,51 @@ struct AlphaSched<T, kW> {
     }
 };
 
+// AlphaSched for a full window t >= 1 with its scratch stores addressed off wave-uniform bases
+// (TD_SADDR): sa = alpha rows of the window + 6 rows, stm = tempmax rows of the window; va[PH] =
+// this lane's byte offset of its state in a row of phase PH, vtm = its codeword's.  Step K stores
+// alpha at sa + va + (K - 6) rows and tempmax[i] at scratch index i - 1 = stm + vtm + (K - 1) rows.
+#ifndef TD_SADDR
+#define TD_SADDR 1
+#endif
+template <typename T, int K>
+struct AlphaSchedS {
+    static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
+                                               int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
+                                               unsigned vtm)
+    {
+        constexpr int PH = K % 3;
+        const StepIn<T> in = op[K % 3];
+        const T an = dpp<PhaseDpp<PH>::ctrl>(a);
+        T m = vmax(a, an);
+        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+        m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));   // tempmax[i] (:986-993)
+        const T alpha = a - m, ap = an - m;                   // :995-1000
+        const T xs = fma(lc.a_sg[PH], in.gs, alpha);
+        const T xp = fma(lc.a_pg[PH], in.gp, ap);
+        const T d = xp - xs;
+        const LutRow r = lut_row(d);
+        __builtin_amdgcn_sched_barrier(0);
+        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+        __builtin_amdgcn_sched_barrier(0);
+        gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
+        gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
+        __builtin_amdgcn_sched_barrier(0);
+        a = sched_finish(xs, xp, d, thr, lo, hi);
+        AlphaSchedS<T, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+    }
+};
+template <typename T>
+struct AlphaSchedS<T, kW> {
+    static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
+                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned)
+    {
+    }
+};
+static_assert(6 * kLanes * 8 <= 4096 && (kW - 7) * kLanes * 8 < 4096, "scheduled alpha store offsets fit the immediate");
+
 // TD_BETA_SHADOW: each beta step writes its incoming beta[.][i+1] (the fold input of step i) into
 // the window's Bv rows behind its own row read, instead of the 12 writes (and their rotated
 // addresses) after the window, which the chain waited for at the window's barrier.
@@ -1128,7 +1189,47 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                           ga0 + (size_t)(t + 1) * kW * kLanes, gtm0 + (size_t)(t + 1) * kW * kCw,
                                           st ? st + 4 : nullptr);
 #else
-        for (int t = 0; t < nT; ++t) {
+        int t0 = 0;
+        if constexpr (ALGO == 0 && TD_SCHED && TD_SADDR) {
+            // windows 1 .. tl-1 are full: running bases and slot index, no per-window address math
+            if (tl >= 2) {
+                TD_STAMP(f0);
+                a = alpha_window<T, ALGO>(a, 0, kW, sm, lut_col(sm, lane), c, lc, ga0, gtm0, st ? st + 4 : nullptr);
+                TD_STAMP(f1);
+                wg_sync_lds();
+                TD_STAMP(f2);
+                TD_ACC(0, f0, f1);
+                TD_ACC(1, f1, f2);
+                const unsigned va[3] = {(unsigned)(lc.st_off[0] * sizeof(T)), (unsigned)(lc.st_off[1] * sizeof(T)),
+                                        (unsigned)(lc.st_off[2] * sizeof(T))};
+                const unsigned vtm = (unsigned)(c * sizeof(T));
+                T* sa = ga0 + (size_t)(kW + 6) * kLanes;
+                T* stm = gtm0 + (size_t)kW * kCw;
+                const T* lut = lut_col(sm, lane);
+                unsigned long long* chain_st = st ? st + 4 : nullptr;
+                (void)chain_st;
+                int tb = 1;
+                for (int t = 1; t < tl; ++t) {
+                    TD_STAMP(f0);
+                    StepIn<T> op[3];
+                    op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
+                    op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
+                    TD_CHAIN_T0(c0);
+                    AlphaSchedS<T, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+                    TD_CHAIN_ACC(c0);
+                    sa += (size_t)kW * kLanes;
+                    stm += (size_t)kW * kCw;
+                    tb = tb == 2 ? 0 : tb + 1;
+                    TD_STAMP(f1);
+                    wg_sync_lds();
+                    TD_STAMP(f2);
+                    TD_ACC(0, f0, f1);
+                    TD_ACC(1, f1, f2);
+                }
+                t0 = tl;
+            }
+        }
+        for (int t = t0; t < nT; ++t) {
             TD_STAMP(f0);
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
                                       ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
@@ -1246,7 +1347,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = 0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wb = tl - j + 1;
-            if (wb >= 0 && wb <= tl) beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc,
+#ifdef TD_DIAG_NOBETA   // diagnostics only (wrong results): the B pass without the beta chain
+            if (false)
+#else
+            if (wb >= 0 && wb <= tl)
+#endif
+                beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc,
                                                                         st ? st + 4 : nullptr);
             TD_STAMP(b1);
             wg_sync_lds();
