@@ -1140,6 +1140,55 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     }
 }
 
+// fold_item for the turbo decode's full windows (TD_FOLD_FAST): the lane's LDS rows and output
+// bases are set up once per SISO, the window enters only as its ring slots (s3 = t % 3, s4 = t %
+// kAvSlots, s2 = t & 1, kept as running counters by the caller) and its first step i0.  Extrinsic
+// written permuted (ext_mode 2 / 3), no raw-LLR or Le dump (those take fold_item).
+#ifndef TD_FOLD_FAST
+#define TD_FOLD_FAST 1
+#endif
+template <typename T>
+struct FoldLane {
+    int k, c;
+    const T* G;      // &sm.G[0][k][c][0]
+    const int* Wp;   // &sm.Wp[0][k][c][0]
+    const T* Bv;     // &sm.Bv[0][k][c * 8]
+    const T* Av;     // &sm.Av[0][k][c * 8]
+    T* ext;          // this codeword's extrinsic row base
+    uint8_t* bits;   // this codeword's decision row (nullptr: none)
+};
+template <typename T, int ALGO>
+__device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* lut, int s3, int s4, int s2, int i0,
+                                               int ext_len, int K)
+{
+    const int k = fl.k;
+    const T* g = fl.G + s3 * (kW * kCw * 4);
+    const T P = g[0], Q = g[1], ys = g[2], la = g[3];
+    const int* wp = fl.Wp + s3 * (kW * kCw * 2);
+    const int wperm = wp[0], wbit = wp[1];
+    T a[8], b[8], t0[8], t1[8];
+    load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
+    load_block<T>(fl.Av + s4 * (kW * kLanes), k, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
+        t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
+    }
+    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
+    T r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
+#pragma unroll
+    for (int j = 2; j < 8; ++j) {
+        r0 = mstar<T, ALGO>(r0, t0[j], lut);
+        r1 = mstar<T, ALGO>(r1, t1[j], lut);
+    }
+    const T llr = r1 - r0;
+    const T le = llr - la - (T)2 * ys;
+    const int i = i0 + k;
+    if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
+    if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
+}
+
 #ifdef TD_STAMPS
 // diagnostic build only: per-wave cycle totals (s_memtime, shader clock)
 #define TD_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -1363,7 +1412,52 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     } else {
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         const int fe = (wave == 0 ? 0 : kFoldPerWave) + lane;
-        for (int j = 0; j < nB; ++j) {
+        int j0 = 0;
+        if (TD_FOLD_FAST && ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
+            // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
+            // here iterations 3 .. nB-1, i.e. the full windows wf = tl-1 .. 0
+            for (int j = 0; j < 3; ++j) {
+                TD_STAMP(b0);
+                const int wf = tl - j + 2;
+                if (lane < kFoldPerWave && wf <= tl && (fe >> 3) < window_len(gm, wf))
+                    fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
+                TD_STAMP(b1);
+                wg_sync_lds();
+                TD_STAMP(b2);
+                TD_ACC(2, b0, b1);
+                TD_ACC(3, b1, b2);
+            }
+            FoldLane<T> fl;
+            fl.k = fe >> 3;
+            fl.c = fe & 7;
+            const int ke = min(fl.k, kW - 1);   // spare lanes: any valid row (they fold nothing)
+            fl.G = &sm.G[0][ke][fl.c][0];
+            fl.Wp = &sm.Wp[0][ke][fl.c][0];
+            fl.Bv = &sm.Bv[0][ke][fl.c * 8];
+            fl.Av = &sm.Av[0][ke][fl.c * 8];
+            fl.ext = dst.ext + (size_t)gm.g * dst.ext_len * kCw + fl.c;
+            const int b_ = gm.g * kCw + fl.c;
+            fl.bits = (dst.bits && b_ < gm.B) ? dst.bits + (size_t)b_ * dst.bits_stride + (size_t)dst.bits_row * gm.K
+                                              : nullptr;
+            const T* lut = lut_col(sm, lane);
+            int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
+            for (int j = 3; j < nB; ++j, --wf) {
+                TD_STAMP(b0);
+#ifndef TD_DIAG_NOFOLD
+                if (lane < kFoldPerWave) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
+#endif
+                s3 = s3 == 0 ? 2 : s3 - 1;
+                s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
+                s2 ^= 1;
+                TD_STAMP(b1);
+                wg_sync_lds();
+                TD_STAMP(b2);
+                TD_ACC(2, b0, b1);
+                TD_ACC(3, b1, b2);
+            }
+            j0 = nB;
+        }
+        for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
 #ifndef TD_DIAG_NOFOLD   // diagnostics only: the B pass without its folds (wrong results)
