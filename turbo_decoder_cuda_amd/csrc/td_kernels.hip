@@ -812,7 +812,12 @@ struct AlphaSched<T, kW> {
 #ifndef TD_SADDR
 #define TD_SADDR 1
 #endif
-template <typename T, int K>
+#ifndef TD_SCHED_MAXLOG
+#define TD_SCHED_MAXLOG 1   // fp64 Max-Log-MAP full windows through AlphaSchedS as well: 1930 -> 2050
+                            // Mbit/s on one box; fp32 Max-Log-MAP lost 23 % with it (2380 -> 1827), so
+                            // it keeps alpha_window's pinned step groups
+#endif
+template <typename T, int ALGO, int K>
 struct AlphaSchedS {
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
                                                int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
@@ -827,22 +832,33 @@ struct AlphaSchedS {
         const T alpha = a - m, ap = an - m;                   // :995-1000
         const T xs = fma(lc.a_sg[PH], in.gs, alpha);
         const T xp = fma(lc.a_pg[PH], in.gp, ap);
-        const T d = xp - xs;
-        const LutRow r = lut_row(d);
-        __builtin_amdgcn_sched_barrier(0);
-        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
-        __builtin_amdgcn_sched_barrier(0);
-        gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
-        gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
-        __builtin_amdgcn_sched_barrier(0);
-        a = sched_finish(xs, xp, d, thr, lo, hi);
-        AlphaSchedS<T, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+        if constexpr (ALGO == 0) {
+            const T d = xp - xs;
+            const LutRow r = lut_row(d);
+            __builtin_amdgcn_sched_barrier(0);
+            const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
+            gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
+            __builtin_amdgcn_sched_barrier(0);
+            a = sched_finish(xs, xp, d, thr, lo, hi);
+        } else {
+            // Max-Log-MAP: no table; alpha stored at the checkpoint phases only (kCkPhases)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((kCkPhases >> PH) & 1) gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
+            gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
+            __builtin_amdgcn_sched_barrier(0);
+            a = vmax(xs, xp);
+        }
+        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
     }
 };
-template <typename T>
-struct AlphaSchedS<T, kW> {
+template <typename T, int ALGO>
+struct AlphaSchedS<T, ALGO, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
                                                const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned)
     {
@@ -1239,7 +1255,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                           st ? st + 4 : nullptr);
 #else
         int t0 = 0;
-        if constexpr (ALGO == 0 && TD_SCHED && TD_SADDR) {
+        if constexpr ((ALGO == 0 || (TD_SCHED_MAXLOG && sizeof(T) == 8)) && TD_SCHED && TD_SADDR) {
             // windows 1 .. tl-1 are full: running bases and slot index, no per-window address math
             if (tl >= 2) {
                 TD_STAMP(f0);
@@ -1264,7 +1280,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
                     TD_CHAIN_T0(c0);
-                    AlphaSchedS<T, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
                     TD_CHAIN_ACC(c0);
                     sa += (size_t)kW * kLanes;
                     stm += (size_t)kW * kCw;
@@ -1545,6 +1561,9 @@ struct WgPos {
 #ifndef TD_ROLE_MAP
 #define TD_ROLE_MAP 2
 #endif
+#ifndef TD_SLOT_XOR
+#define TD_SLOT_XOR 2   // map 2: the second workgroup's role on a SIMD = first's ^ 2 (A/F0, B/F1); 3: A/F1, B/F0
+#endif
 __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1572,7 +1591,7 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
             for (int b = a + 1; b < kWaves; ++b) distinct = distinct && s_simd[a] != s_simd[b];
         const int slot = s_slot;
         const int base = distinct ? simd : wave;
-        return WgPos{h, slot == 1 ? base ^ 2 : base, lane, g, key, slot};
+        return WgPos{h, slot == 1 ? base ^ TD_SLOT_XOR : base, lane, g, key, slot};
     }
     const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
     int role;
