@@ -812,6 +812,9 @@ struct AlphaSched<T, kW> {
 #ifndef TD_SADDR
 #define TD_SADDR 1
 #endif
+#ifndef TD_LOADER_PRIO_MAXLOG
+#define TD_LOADER_PRIO_MAXLOG 0   // VALU priority of the loader wave in the Max-Log-MAP B pass
+#endif
 #ifndef TD_SCHED_MAXLOG
 #define TD_SCHED_MAXLOG 1   // fp64 Max-Log-MAP full windows through AlphaSchedS as well: 1930 -> 2050
                             // Mbit/s on one box; fp32 Max-Log-MAP lost 23 % with it (2380 -> 1827), so
@@ -1355,6 +1358,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // own and the previous iteration's DMAs in flight: three windows of latency for each.
         constexpr int kB = kF + 1 + alpha_dma_count<T, ALGO>();
         vm_wait<0>();   // the F pass's last (unused) staging
+        if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
         auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
             const int wa = tl - j;
