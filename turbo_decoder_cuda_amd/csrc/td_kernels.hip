@@ -1194,6 +1194,12 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
         t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
         t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
     }
+#ifdef TD_DIAG_HALFFOLD   // diagnostics only (wrong results): one E_seq chain per item
+    T r0 = mstar<T, ALGO>(t0[0], t1[1], lut);
+#pragma unroll
+    for (int j = 2; j < 8; ++j) r0 = mstar<T, ALGO>(r0, t0[j] + t1[j], lut);
+    const T r1 = P;
+#else
     T r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
     T r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
 #pragma unroll
@@ -1201,6 +1207,7 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
         r0 = mstar<T, ALGO>(r0, t0[j], lut);
         r1 = mstar<T, ALGO>(r1, t1[j], lut);
     }
+#endif
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
     const int i = i0 + k;
@@ -1943,10 +1950,16 @@ __global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs
     }
 }
 
+#ifndef TD_SW_SEG_F64
+#define TD_SW_SEG_F64 4   // 2 (4 waves/SIMD, half the recompute, twice the checkpoint traffic) measured -12 %
+#endif
+#ifndef TD_SW_SEG_F32
+#define TD_SW_SEG_F32 8
+#endif
 template <typename T>
 constexpr int sw_seg()
 {
-    return sizeof(T) == 4 ? 8 : 4;   // checkpoint spacing S: the segment's alpha stays in registers
+    return sizeof(T) == 4 ? TD_SW_SEG_F32 : TD_SW_SEG_F64;   // checkpoint spacing S: the segment's alpha stays in registers
 }
 
 template <typename T, int ALGO>
