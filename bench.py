@@ -13,7 +13,8 @@ Extra objects on the JSON line:
   roofline      the turbo kernel against HBM (algorithmic bytes: fp64 LLR in + uint8 bits out
                 per codeword) with durations from hipEvents inside the timed region;
                 `traffic` from the committed rocprofv3 PMC profile of the same config (or null)
-  cpu_baseline  oracle/ (CPU restatement of log_map.cpp, fp64) on the host cores, rank 0, N=1
+  cpu_baseline  the compiled reference (oracle/_ref/ref_harness: ITTC/log_map.cpp's SISO and loop) on the
+                host cores, rank 0, N=1; the C restatement (oracle/) where that binary is absent
   variants      fp32 log-MAP, fp64/fp32 Max-Log-MAP on the same batch (fewer steps)
 """
 from __future__ import annotations
@@ -223,14 +224,41 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     }
 
 
+REF_HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+
+
 def cpu_baseline(a, llr_h, gpu_bits, f1, f2):
-    """The CPU restatement of log_map.cpp (oracle/, fp64 table log-MAP -- the reference's own
-    arithmetic) on the host cores, over the first `cpu_sample` codewords of the same batch."""
+    """The reference's CPU path on the host cores, over the first `cpu_sample` codewords of the
+    same batch.  fp64 log-MAP: the compiled reference itself (oracle/_ref/ref_harness, built from
+    /root/reference/ITTC/log_map.cpp by `make -C oracle ref`; its `decode` mode runs TurboDecoding's
+    loop through the reference's functions, frames spread over threads) -- kind "reference".
+    Otherwise, or where that binary was not built: the C restatement (oracle/) -- kind "port"."""
+    n = min(a.cpu_sample, a.batch)
+    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    if a.precision == "f64" and a.algo == "logmap" and os.access(REF_HARNESS, os.X_OK):
+        import subprocess
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as td:
+            fin, fout = os.path.join(td, "flows.bin"), os.path.join(td, "bits.bin")
+            np.ascontiguousarray(llr_h[:n], dtype=np.float64).tofile(fin)
+            r = subprocess.run([REF_HARNESS, "decode", str(a.K), str(f1), str(f2), str(a.iters), str(threads), fin, fout],
+                               capture_output=True, text=True, check=True)
+            dt = float(r.stdout.split()[1])
+            cb = np.fromfile(fout, dtype=np.uint8).reshape(n, a.K)
+        return {
+            "value": round(n * a.K / dt / 1e6, 4),
+            "unit": "Mbit/s",
+            "cores": threads,
+            "kind": "reference",
+            "sample": f"{n} codewords of the same batch (K={a.K}, {a.iters} iter, fp64 log-MAP) through the compiled "
+                      f"reference (ITTC/log_map.cpp, g++ -O2), {threads} threads, {dt:.2f} s",
+            "bits_match_gpu": bool(np.array_equal(cb, gpu_bits[:n])),
+            "cpu_model": _cpu_model(),
+        }
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
 
-    n = min(a.cpu_sample, a.batch)
-    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
     sample = np.ascontiguousarray(llr_h[:n])
     if a.precision == "f32":
         sample = sample.astype(np.float32)

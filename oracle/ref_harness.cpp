@@ -12,7 +12,13 @@
 //   time K f1 f2 nframes                          -- ms per TurboDecoding call (15 iterations)
 //   demod M nsym seed out                         -- demodule() on random + constellation-point symbols
 //   framesmod K f1 f2 M ebn0 seed nframes out     -- main.cpp frames with MODULATION = M (src, flow)
+//   decode K f1 f2 iters nthreads in out          -- the CPU baseline of bench.py: frames read from `in`
+//                                                    (nframes x (3K+12) doubles) decoded through the
+//                                                    reference's functions in TurboDecoding's order,
+//                                                    frames spread over threads; writes the last
+//                                                    iteration's bits (uint8) and prints the wall time
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -289,6 +295,68 @@ static int mode_demod(int argc, char** argv)
     return 0;
 }
 
+// TurboDecoding (log_map.cpp:1146-1280) with `iters` iterations instead of the N_ITERATION
+// macro, on many frames: the same loop as replay() minus the Le dumps.  The reference is
+// re-entrant after TurboCodingInit (read-only globals, per-call mallocs), so threads decode
+// frames round-robin.  Output: the hard bits after the last iteration (uint8, natural order).
+static void decode_one(int K, const double* flow_in, int iters, unsigned char* out)
+{
+    const int L = K + M_num_reg, n = 3 * K + 4 * M_num_reg;
+    std::vector<double> flow(flow_in, flow_in + n), yk(4 * L), La(L, 0.0), Le(L, 0.0), LLR(L, 0.0);
+    std::vector<int> tempout(L), bits(K);
+    for (int i = 0; i < n; i++) flow[i] *= 0.5;
+    demultiplex(flow.data(), K, yk.data());
+    for (int it = 0; it < iters; it++) {
+        random_deinterlvr_double(La.data(), Le.data(), index_randomintlvr, K);
+        for (int i = K; i < L; i++) La[i] = 0;
+        Log_MAP_decoder(yk.data(), La.data(), 1, LLR.data(), L);
+        for (int i = 0; i < L; i++) Le[i] = LLR[i] - La[i] - 2 * (yk[2 * i]);
+        randominterleaver_double(Le.data(), La.data(), index_randomintlvr, K);
+        for (int i = K; i < L; i++) La[i] = 0;
+        Log_MAP_decoder(yk.data() + 2 * L, La.data(), 1, LLR.data(), L);
+        for (int i = 0; i < L; i++) Le[i] = LLR[i] - La[i] - 2 * (yk[2 * L + 2 * i]);
+        decision(LLR.data(), L, tempout.data());
+        random_deinterlvr_int(bits.data(), tempout.data(), index_randomintlvr, K);
+    }
+    for (int i = 0; i < K; i++) out[i] = (unsigned char)bits[i];
+}
+
+static int mode_decode(int argc, char** argv)
+{
+    if (argc != 9) return 2;
+    int K = atoi(argv[2]), a = atoi(argv[3]), b = atoi(argv[4]), iters = atoi(argv[5]), nt = atoi(argv[6]);
+    setup(K, a, b);
+    const size_t n = 3 * (size_t)K + 12;
+    FILE* fi = fopen(argv[7], "rb");
+    if (!fi) {
+        perror(argv[7]);
+        return 2;
+    }
+    std::vector<double> flows;
+    {
+        std::vector<double> buf(n);
+        while (fread(buf.data(), sizeof(double), n, fi) == n) flows.insert(flows.end(), buf.begin(), buf.end());
+    }
+    fclose(fi);
+    const int nf = (int)(flows.size() / n);
+    if (nt < 1) nt = 1;
+    std::vector<unsigned char> out((size_t)nf * K);
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            for (int fr = t; fr < nf; fr += nt) decode_one(K, flows.data() + (size_t)fr * n, iters, out.data() + (size_t)fr * K);
+        });
+    for (auto& x : th) x.join();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    FILE* f = must_open(argv[8]);
+    fwrite(out.data(), 1, out.size(), f);
+    fclose(f);
+    printf("seconds %.6f frames %d threads %d\n", sec, nf, nt);
+    TurboCodingRelease();
+    return 0;
+}
+
 // main.cpp:170-202 frames with MODULATION = M: src [K] int32 + flow [3K+12] double per frame
 static int mode_framesmod(int argc, char** argv)
 {
@@ -323,6 +391,7 @@ int main(int argc, char** argv)
     if (!strcmp(argv[1], "time")) return mode_time(argc, argv);
     if (!strcmp(argv[1], "demod")) return mode_demod(argc, argv);
     if (!strcmp(argv[1], "framesmod")) return mode_framesmod(argc, argv);
+    if (!strcmp(argv[1], "decode")) return mode_decode(argc, argv);
     fprintf(stderr, "unknown mode\n");
     return 2;
 }

@@ -132,3 +132,25 @@ def test_modulate_demodulate_round_trip(M):
     si, sq = O.modulate(bits, M)
     llr = O.demodulate(si, sq, M, 1.0)
     assert np.array_equal((llr > 0).astype(int), bits)
+
+
+REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "ref_harness")
+
+
+@pytest.mark.skipif(not os.access(REF_HARNESS, os.X_OK), reason="compiled reference not built here (make -C oracle ref)")
+def test_reference_decode_mode_matches_oracle(tmp_path):
+    """bench.py's CPU baseline runs the compiled reference's `decode` mode (TurboDecoding's loop
+    through log_map.cpp's own functions, frames over threads): its bits equal the restatement's."""
+    import subprocess
+
+    from turbo_decoder_cuda_amd import synth
+
+    u, llr = synth.make_batch(6, 1024, 31, 64, 0.5, seed=3, dtype=np.float64)
+    fin, fout = str(tmp_path / "flows.bin"), str(tmp_path / "bits.bin")
+    llr.tofile(fin)
+    r = subprocess.run([REF_HARNESS, "decode", "1024", "31", "64", "4", "3", fin, fout], capture_output=True,
+                       text=True, check=True)
+    assert r.stdout.startswith("seconds ") and " frames 6 " in r.stdout
+    rb = np.fromfile(fout, dtype=np.uint8).reshape(6, 1024)
+    ob = O.decode_batch(np.ascontiguousarray(llr), 1024, 31, 64, 4, O.ALGO_LOGMAP, nthreads=2)
+    assert np.array_equal(rb, ob)
