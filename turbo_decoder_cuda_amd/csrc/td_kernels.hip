@@ -815,6 +815,9 @@ struct AlphaSched<T, kW> {
 #ifndef TD_LOADER_PRIO_MAXLOG
 #define TD_LOADER_PRIO_MAXLOG 0   // VALU priority of the loader wave in the Max-Log-MAP B pass
 #endif
+#ifndef TD_AOP_FIRST
+#define TD_AOP_FIRST 1
+#endif
 #ifndef TD_SCHED_MAXLOG
 #define TD_SCHED_MAXLOG 1   // fp64 Max-Log-MAP full windows through AlphaSchedS as well: 1930 -> 2050
                             // Mbit/s on one box; fp32 Max-Log-MAP lost 23 % with it (2380 -> 1827), so
@@ -1289,6 +1292,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     StepIn<T> op[3];
                     op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
+                    if (TD_AOP_FIRST) __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
                     TD_CHAIN_T0(c0);
                     AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
                     TD_CHAIN_ACC(c0);
