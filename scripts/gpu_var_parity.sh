@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU box job: the parity tests (TESTS, default test_gpu_parity.py) against every libvar_*.so.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+for lib in turbo_decoder_cuda_amd/libvar_*.so; do
+  TD_LIB_PATH=$PWD/$lib timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py} -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/vp.log 2>&1
+  echo "$(basename $lib): rc=$? $(tail -1 gpurun_out/vp.log)"
+done

@@ -998,8 +998,10 @@ constexpr bool kBetaBatch = TD_BETA_BATCH != 0;   // beta published once per win
 template <typename T, int ALGO>
 constexpr bool kBetaPin = TD_BETA_PIN != 0 && (sizeof(T) == 8 || ALGO == 0);
 
-// beta over the n steps of window t, downwards (full windows: static phases; else runtime)
-template <typename T, int ALGO>
+// beta over the n steps of window t, downwards (full windows: static phases; else runtime).
+// FULL = false keeps only the rolled runtime-phase loop (the last window in the dedicated loop of
+// the B pass, so that the unrolled full-window code exists once in the kernel)
+template <typename T, int ALGO, bool FULL = true>
 __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, const T* lut, int c, const LaneConst<T>& lc,
                                          unsigned long long* chain_st = nullptr)
 {
@@ -1007,6 +1009,14 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
     const int tb = t % 3, xb = t & 1;
     T* Bvw = &sm.Bv[xb][0][0];
     const T* tmw = &sm.tm[xb][0][0];
+    if constexpr (!FULL) {
+        for (int k = n - 1; k >= 0; --k) {
+            const int ph1 = (k + 1) % 3;   // constant indices only: a runtime index into lc moves it to scratch
+            Bvw[k * kLanes + rot_off<T>(ph1 == 0 ? lc.st_off[0] : ph1 == 1 ? lc.st_off[1] : lc.st_off[2], k)] = beta;
+            beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, tmw);
+        }
+        return beta;
+    }
 #if TD_SCHED
     if (ALGO == 0 && n == kW) {
         T bs[kW];   // beta[.][i+1] of step k, published after the window
@@ -1064,6 +1074,31 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
             beta = beta_step_rt<T, ALGO>(k % 3, beta, sm, lut, tb, k, c, lc, tmw);
         }
     }
+    return beta;
+}
+
+// beta_window's scheduled path for a full window whose ring slots the caller keeps as running
+// counters (tb = t % 3, xb = t & 1): no window-length test, no modular arithmetic (TD_BETA_FAST)
+#ifndef TD_BETA_FAST
+#define TD_BETA_FAST 1
+#endif
+template <typename T, int ALGO>
+__device__ __forceinline__ T beta_window_full(T beta, int tb, int xb, Smem<T>& sm, const T* lut, int c,
+                                              const LaneConst<T>& lc, unsigned long long* chain_st = nullptr)
+{
+    (void)chain_st;
+    T* Bvw = &sm.Bv[xb][0][0];
+    const T* tmw = &sm.tm[xb][0][0];
+    T bs[kW];
+    StepIn<T> op[3];
+    op[(kW - 1) % 3] = beta_in<T, (kW - 1) % 3>(sm, tb, kW - 1, c, lc, tmw);
+    op[(kW - 2) % 3] = beta_in<T, (kW - 2) % 3>(sm, tb, kW - 2, c, lc, tmw);
+    TD_CHAIN_T0(c0);
+    BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
+    TD_CHAIN_ACC(c0);
+    if (!TD_BETA_SHADOW)
+#pragma unroll
+        for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
     return beta;
 }
 
@@ -1424,7 +1459,39 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         lane_setup(lt, lane, lc);
         const int phL = gm.L % 3;   // beta[.][L] lives in the labeling of phase L mod 3
         T beta = (src.terminated && !((lc.b_init0 >> phL) & 1)) ? (T)-kInfty : (T)0;   // :944,951-959
-        for (int j = 0; j < nB; ++j) {
+        int j0 = 0;
+        if constexpr (ALGO == 0 && TD_SCHED && TD_BETA_FAST) {
+            if (tl >= 1) {
+                // j = 0 (nothing) and j = 1 (window tl, maybe partial: the rolled loop), then the full
+                // windows wb = tl-1 .. 0 (j = 2 .. nB-2) with running slot counters
+                for (int j = 0; j < 2; ++j) {
+                    TD_STAMP(b0);
+                    if (j == 1)
+                        beta = beta_window<T, ALGO, false>(beta, tl, window_len(gm, tl), sm, lut_col(sm, lane), lane >> 3,
+                                                           lc, st ? st + 4 : nullptr);
+                    TD_STAMP(b1);
+                    wg_sync_lds();
+                    TD_STAMP(b2);
+                    TD_ACC(2, b0, b1);
+                    TD_ACC(3, b1, b2);
+                }
+                const T* lut = lut_col(sm, lane);
+                int tb = (tl - 1) % 3, xb = (tl - 1) & 1;
+                for (int wb = tl - 1; wb >= 0; --wb) {
+                    TD_STAMP(b0);
+                    beta = beta_window_full<T, ALGO>(beta, tb, xb, sm, lut, lane >> 3, lc, st ? st + 4 : nullptr);
+                    tb = tb == 0 ? 2 : tb - 1;
+                    xb ^= 1;
+                    TD_STAMP(b1);
+                    wg_sync_lds();
+                    TD_STAMP(b2);
+                    TD_ACC(2, b0, b1);
+                    TD_ACC(3, b1, b2);
+                }
+                j0 = tl + 2;   // j = nB - 1 (wb = -1): beta idle, the folds finish window 0
+            }
+        }
+        for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wb = tl - j + 1;
 #ifdef TD_DIAG_NOBETA   // diagnostics only (wrong results): the B pass without the beta chain
