@@ -823,11 +823,40 @@ struct AlphaSched<T, kW> {
                             // Mbit/s on one box; fp32 Max-Log-MAP lost 23 % with it (2380 -> 1827), so
                             // it keeps alpha_window's pinned step groups
 #endif
+// TD_TM_BATCH: the 8 lanes of a codeword hold the same tempmax, so instead of a store per step each
+// lane keeps the tempmax of one step (lane slot l: steps l and 8 + (l & 3) of the window) and the
+// window writes them with two stores (steps 0-7, then 8-11; lanes l and l + 4 write the same value
+// twice in the second): 2 scratch stores a window instead of 12 beside the recursion.
+#ifndef TD_TM_BATCH
+#define TD_TM_BATCH 1
+#endif
+static_assert(kW == 12, "the tempmax batches cover a window of 8 + 4 steps");
+template <typename T>
+struct TmBatch {
+    T buf;
+    int slot;          // lane & 7
+    unsigned v1, v2;   // byte offsets of this lane's entry in the first / second batch
+};
+template <typename T, int K>
+__device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm, unsigned vtm)
+{
+    if constexpr (TD_TM_BATCH) {
+        if constexpr (K < 8)
+            tbh.buf = tbh.slot == K ? m : tbh.buf;
+        else
+            tbh.buf = (tbh.slot & 3) == K - 8 ? m : tbh.buf;
+        if constexpr (K == 7) gstore_s<-kCw * (int)sizeof(T)>(stm, tbh.v1, tbh.buf);           // steps 0-7 at i - 1
+        if constexpr (K == kW - 1) gstore_s<7 * kCw * (int)sizeof(T)>(stm, tbh.v2, tbh.buf);   // steps 8-11
+    } else {
+        gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);   // tempmax[i] at scratch index i - 1
+    }
+}
+
 template <typename T, int ALGO, int K>
 struct AlphaSchedS {
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
                                                int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
-                                               unsigned vtm)
+                                               unsigned vtm, TmBatch<T>& tbh)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -847,7 +876,7 @@ struct AlphaSchedS {
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
             gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
-            gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
+            tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
         } else {
@@ -856,17 +885,17 @@ struct AlphaSchedS {
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr ((kCkPhases >> PH) & 1) gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
-            gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);
+            tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
         }
-        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh);
     }
 };
 template <typename T, int ALGO>
 struct AlphaSchedS<T, ALGO, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned)
+                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned, TmBatch<T>&)
     {
     }
 };
@@ -1316,6 +1345,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 const unsigned va[3] = {(unsigned)(lc.st_off[0] * sizeof(T)), (unsigned)(lc.st_off[1] * sizeof(T)),
                                         (unsigned)(lc.st_off[2] * sizeof(T))};
                 const unsigned vtm = (unsigned)(c * sizeof(T));
+                TmBatch<T> tbh{(T)0, lane & 7, (unsigned)(((lane & 7) * kCw + c) * sizeof(T)),
+                               (unsigned)(((lane & 3) * kCw + c) * sizeof(T))};
                 T* sa = ga0 + (size_t)(kW + 6) * kLanes;
                 T* stm = gtm0 + (size_t)kW * kCw;
                 const T* lut = lut_col(sm, lane);
@@ -1329,7 +1360,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
                     if (TD_AOP_FIRST) __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
                     TD_CHAIN_T0(c0);
-                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm);
+                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh);
                     TD_CHAIN_ACC(c0);
                     sa += (size_t)kW * kLanes;
                     stm += (size_t)kW * kCw;
