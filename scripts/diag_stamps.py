@@ -48,7 +48,9 @@ print(f"  clock {clk:.3f} GHz; kernel {kc.mean() / steps:.1f} cycles per SISO-st
       f"{acc.mean() / steps:.1f} (unstamped: SISO prologues / epilogues, {(kc.mean() - acc.mean()) / steps:.1f})")
 for w in range(4):
     print(f"  {roles[w]:14s} per SISO-step: SISO calls {s[:, w, 9].mean() / steps:7.1f}  SISO-end barrier "
-          f"{s[:, w, 10].mean() / steps:6.1f}  in-SISO unstamped {(s[:, w, 9] - s[:, w, 0:4].sum(axis=1)).mean() / steps:6.1f}")
+          f"{s[:, w, 10].mean() / steps:6.1f}  in-SISO unstamped {(s[:, w, 9] - s[:, w, 0:4].sum(axis=1)).mean() / steps:6.1f}"
+          + (f"  F prologue {s[:, w, 11].mean() / steps:6.1f}" if NS > 11 else "")
+          + (f"  B prologue {s[:, w, 12].mean() / steps:6.1f}  first tile {s[:, w, 13].mean() / steps:6.1f}" if NS > 13 and w == 2 else ""))
 hw = st.cpu().numpy().reshape(G, 4, NS)[:, :, 6].astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15

@@ -660,7 +660,7 @@ int td_debug_set_stamps(td_handle* h, void* d_buf)
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
-    return 4 * 11;   // [wave][slot] (td_kernels.hip kStampSlots)
+    return 4 * 14;   // [wave][slot] (td_kernels.hip kStampSlots)
 #else
     return 0;
 #endif

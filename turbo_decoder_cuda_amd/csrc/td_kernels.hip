@@ -1290,9 +1290,9 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #define TD_STAMP(v)
 #define TD_ACC(slot, a, b)
 #endif
-constexpr int kStampSlots = 11;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
+constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
-                                 // barriers (see diag)
+                                 // barriers, F prologue, loader B prologue, loader first tile (see diag)
 
 // The loader wave keeps one register set per stream, issued one iteration ahead and consumed
 // (stored to LDS) at the start of the next iteration before it is re-issued; it issues the same
@@ -1307,6 +1307,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                         T* tmstore, const LaneTables* lt, int wave, int lane, unsigned long long* st)
 {
     (void)st;
+    TD_STAMP(p0);
     const int nT = gm.nT;
     const int tl = nT - 1;
     const int nB = nT + 2;   // B-pass iterations: j = 0 .. nT+1 (wa = tl - j, wb = wa + 1, wf = wa + 2)
@@ -1321,6 +1322,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         T a = lc.a_init0 ? (T)0 : (T)-kInfty;   // alpha[.][0] (:943,948), its tempmax is 0
         __builtin_amdgcn_s_setprio(2);
         wg_sync_lds();
+        TD_STAMP(p1);
+        TD_ACC(11, p0, p1);
 #ifdef TD_DIAG_FPAIR   // diagnostics only (wrong results): two alpha windows per F-pass barrier (on one tile)
         for (int t = 0; t < nT; t += 2) {
             TD_STAMP(f0);
@@ -1416,11 +1419,15 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         };
         tile_dma(sm, 0, src, dst, gm, 0, lane);
         vm_wait<0>();
+        TD_STAMP(p2);
+        TD_ACC(13, p0, p2);
         tile_convert(sm, 0, src, 0, lane);
         tile_dma(sm, 1, src, dst, gm, min(1, tl), lane);
         tile_dma(sm, 2, src, dst, gm, min(2, tl), lane);
         vm_wait<kF>();
         wg_sync_lds();
+        TD_STAMP(p1);
+        TD_ACC(11, p0, p1);
 #ifdef TD_DIAG_FPAIR
         for (int t = 0; t < nT; t += 2) fstep(t);
 #else
@@ -1434,6 +1441,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
         // own and the previous iteration's DMAs in flight: three windows of latency for each.
         constexpr int kB = kF + 1 + alpha_dma_count<T, ALGO>();
+        TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
         if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
         auto bstep = [&](int j, int slot) {
@@ -1460,6 +1468,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         tm_dma(sm, 2, tmstore, gm, tl - 2, lane);
         alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);          // folded at j = 2
         vm_wait<2 * (kF + 1) + alpha_dma_count<T, ALGO>()>();   // slot 0 landed
+        TD_STAMP(p4);
+        TD_ACC(12, p3, p4);
         for (int j = 0; j < nB; j += 3) {
             bstep(j, 0);
             if (j + 1 < nB) bstep(j + 1, 1);
@@ -1469,6 +1479,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         return;
     } else {
         wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
+        TD_STAMP(p1);
+        TD_ACC(11, p0, p1);
 #ifdef TD_DIAG_FPAIR
         for (int t = 0; t < nT; t += 2) {
 #else
