@@ -101,7 +101,8 @@ def main():
     codec = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=local)
     if a.window:
         codec.set_window(a.window, a.overlap)
-    codec.reserve(a.batch)
+    codec.reserve(a.batch)   # also picks the workspace placement (td_reserve)
+    placement = codec.placement()
     bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -129,6 +130,8 @@ def main():
     blk = int((bits != u_d).any(dim=1).sum().item())
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
     out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
+    out["workspace_placement"] = {"probe_ms": placement[0], "kept": placement[1],
+                                  "note": "one-iteration probe per candidate workspace at td_reserve (outside the timed region)"}
 
     if rank == 0 and world == 1 and not a.no_variants:
         out["pcie_inclusive"] = pcie_inclusive(a, codec, llr, dev, stream)

@@ -64,6 +64,11 @@ int td_destroy(td_handle* h);
  * synchronises the device; call td_reserve (after td_set_window) before a decode is captured
  * into a hipGraph. */
 int td_reserve(td_handle* h, int B);
+/* td_reserve of the exact schedule for B >= 1024 also picks the workspace's placement: the turbo
+ * kernel's speed depends on the physical pages behind it (two modes 6-7 % apart on MI355X), so it
+ * times one iteration on candidate workspaces (up to TD_PLACEMENT_TRIALS, environment variable,
+ * default 10; 1 = a plain allocation; stopping once both modes were seen) and keeps the fastest.
+ * Results do not depend on it. */
 
 /*
  * Batched TurboDecoding (log_map.cpp:1146-1280) on device-resident data.
@@ -117,6 +122,10 @@ int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launch
  * (uint64).  The production library ignores the buffer and reports 0 slots. */
 int td_debug_set_stamps(td_handle* h, void* d_buf);
 int td_debug_stamp_slots(void);
+/* Workspace placement of the last td_reserve that allocated (see td_reserve): the number of
+ * candidate workspaces timed (0 = plain allocation), their probe times in ms (up to cap of them)
+ * and the index kept. */
+int td_debug_placement(td_handle* h, float* ms, int cap, int* pick);
 
 /* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
  *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)

@@ -36,5 +36,5 @@ for i in range(ninst):
         _, turbo_ms, _n = codec.kernel_ms()
         codec.profile(False)
         row.append("%.2f/%.0f" % (turbo_ms, B * K * steps / dt / 1e6))
-    print("instance", i, "kernel_ms/Mbps per batch:", " ".join(row), flush=True)
+    print("instance", i, "kernel_ms/Mbps per batch:", " ".join(row), "placement", codec.placement(), flush=True)
     keep.append(codec)   # keep the workspace so the next instance gets another allocation

@@ -237,6 +237,14 @@ constexpr int kWaves = 4;                            // waves per codeword group
 constexpr int kGroupsPerWg = TD_GROUPS_PER_WG;
 constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (A and F1) per window
 static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
+// log-MAP: fold items of wave A (its SIMD partner is the other workgroup's loader) per window; F1,
+// which shares its SIMD with the other workgroup's beta, takes the remaining kTile - kFoldA
+#ifndef TD_FOLD_A
+#define TD_FOLD_A 48
+#endif
+template <int ALGO>
+constexpr int kFoldA = ALGO == 0 ? TD_FOLD_A : kFoldPerWave;
+static_assert(TD_FOLD_A <= kLanes && kTile - TD_FOLD_A <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 
 // Loader staging.  Window inputs travel HBM -> LDS by DMA (global_load_lds_dwordx4: no VGPR
@@ -1552,7 +1560,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     } else {
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
-        const int fe = (wave == 0 ? 0 : kFoldPerWave) + lane;
+        const int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
+        const int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
         int j0 = 0;
         if (TD_FOLD_FAST && ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
@@ -1560,7 +1569,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             for (int j = 0; j < 3; ++j) {
                 TD_STAMP(b0);
                 const int wf = tl - j + 2;
-                if (lane < kFoldPerWave && wf <= tl && (fe >> 3) < window_len(gm, wf))
+                if (lane < nfold && wf <= tl && (fe >> 3) < window_len(gm, wf))
                     fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
                 TD_STAMP(b1);
                 wg_sync_lds();
@@ -1585,7 +1594,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
 #ifndef TD_DIAG_NOFOLD
-                if (lane < kFoldPerWave) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
+                if (lane < nfold) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
 #endif
                 s3 = s3 == 0 ? 2 : s3 - 1;
                 s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
@@ -1602,7 +1611,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             TD_STAMP(b0);
             const int wf = tl - j + 2;
 #ifndef TD_DIAG_NOFOLD   // diagnostics only: the B pass without its folds (wrong results)
-            if (lane < kFoldPerWave && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
+            if (lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
 #endif
             TD_STAMP(b1);

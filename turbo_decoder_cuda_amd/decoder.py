@@ -66,6 +66,16 @@ class TurboCodec:
     def reserve(self, B: int) -> None:
         N.check(N.lib().td_reserve(self._h, int(B)))
 
+    def placement(self):
+        """(probe ms of each candidate workspace, index kept) of the last reserve that allocated
+        (td_debug_placement; ([], -1) for a plain allocation)."""
+        ms = (C.c_float * 16)()
+        pick = C.c_int(-1)
+        n = N.lib().td_debug_placement(self._h, ms, 16, C.byref(pick))
+        if n < 0:
+            N.check(n)
+        return [round(ms[i], 4) for i in range(min(n, 16))], pick.value
+
     def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
                    concurrent: bool = False) -> None:
         """Windowed schedule (td_set_window; BASELINE config 5); window=0: exact.
