@@ -1,4 +1,5 @@
-"""Workspace-placement probe (GPU box, TD_WS_EXPERIMENT build via TD_LIB_PATH): for several decoder
+"""Workspace-placement probe (GPU box, a -DTD_WS_EXPERIMENT build via TD_LIB_PATH,
+with TD_PLACEMENT_TRIALS=1): for several decoder
 instances (fresh allocations), the kernel time with the workspace carve shifted by a list of
 offsets inside the same allocation.  Offsets that change the time within an instance point at the
 layout (channel / page mapping of the streams); a time set by the instance alone points at the
@@ -10,6 +11,8 @@ import time
 
 import numpy as np
 import torch
+
+os.environ.setdefault("TD_PLACEMENT_TRIALS", "1")
 
 sys.path.insert(0, ".")
 from turbo_decoder_cuda_amd import TurboCodec, synth  # noqa: E402

@@ -169,6 +169,11 @@ Carve carve(int G, int K, size_t elem)
     c.astore = c.ext21 + arrK;
     c.tmstore = c.astore + arrA;
     c.total = c.tmstore + arrL;
+#ifdef TD_WS_EXPERIMENT   // diagnostics build: gaps (env, bytes) before astore, tmstore and ext12
+    auto gap = [](const char* n) { const char* e = std::getenv(n); return e ? (size_t)std::strtoull(e, nullptr, 0) & ~(size_t)255 : 0; };
+    const size_t ge = gap("TD_WS_GAP_E"), ga = gap("TD_WS_GAP_A"), gt = gap("TD_WS_GAP_T");
+    c.ext12 += ge; c.ext21 += ge; c.astore += ge + ga; c.tmstore += ge + ga + gt; c.total += ge + ga + gt;
+#endif
     return c;
 }
 
@@ -182,7 +187,13 @@ int ensure_ws(td_handle* h, int G)
         h->d_ws = nullptr;
         h->ws_groups = 0;
     }
+#if defined(TD_WS_EXPERIMENT) && defined(TD_WS_CONTIG)   // diagnostics: physically contiguous, slack for the gaps / offset
+    if (hipExtMallocWithFlags(&h->d_ws, c.total + (512u << 20), hipDeviceMallocContiguous) != hipSuccess) {
+#elif defined(TD_WS_EXPERIMENT)
+    if (hipMalloc(&h->d_ws, c.total + (512u << 20)) != hipSuccess) {
+#else
     if (hipMalloc(&h->d_ws, c.total) != hipSuccess) {
+#endif
         h->d_ws = nullptr;
         return fail(TD_ENOMEM, "hipMalloc of the decode workspace failed (" + std::to_string(c.total) + " B)");
     }
@@ -368,6 +379,9 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     if (rc) return rc;
     const Carve c = carve(G, h->p.K, sizeof(T));
     char* ws = static_cast<char*>(h->d_ws);
+#ifdef TD_WS_EXPERIMENT   // diagnostics build: the carve starts TD_WS_OFFSET bytes into the workspace
+    if (const char* o = std::getenv("TD_WS_OFFSET")) ws += std::strtoull(o, nullptr, 0) & ~(size_t)255;
+#endif
     td::DecodeParams<T> dp{};
     fill_common(dp, h);
     dp.sys1 = reinterpret_cast<T*>(ws + c.sys1);
