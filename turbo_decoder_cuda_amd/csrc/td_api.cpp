@@ -240,11 +240,11 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
     // untimed launches first (the first probe of a process also brings the clocks up), then the
     // best of two timed ones
     for (int w = 0; w < warm; ++w)
-        if (td::launch_turbo<T>(dp, st) != hipSuccess) return -1.f;
+        if (td::launch_turbo<T>(dp, st, true) != hipSuccess) return -1.f;
     float best = -1.f;
     for (int r = 0; r < 2; ++r) {
         float ms = -1.f;
-        if (hipEventRecord(e0, st) != hipSuccess || td::launch_turbo<T>(dp, st) != hipSuccess ||
+        if (hipEventRecord(e0, st) != hipSuccess || td::launch_turbo<T>(dp, st, true) != hipSuccess ||
             hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
             hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
             return -1.f;

@@ -63,7 +63,7 @@ template <typename T>
 hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st);
 // the turbo iterations (one wave per 8 codewords)
 template <typename T>
-hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st);
+hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st, bool probe = false);   // probe: td_reserve's placement probe symbol
 
 // sliding-window mode (BASELINE config 5, td_set_window): sub-blocks of `window` steps
 struct WindowParams {

@@ -1750,7 +1750,7 @@ __device__ __forceinline__ void wg_release(const WgPos& w, unsigned* slots)
 
 // The whole turbo decode of 8 codewords per workgroup (TurboDecoding, log_map.cpp:1146-1280).
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
+__device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
 {
     const WgPos w = wg_pos(p.role_cus, p.cu_slots);
     Smem<T>& sm = smem<T>()[w.group];
@@ -1796,6 +1796,22 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
             p.stamps[((size_t)w.g * kWaves + wave) * kStampSlots + q] = st[q];
 #endif
     wg_release(w, p.cu_slots);
+}
+
+template <typename T, int ALGO>
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
+{
+    turbo_decode_body<T, ALGO>(p);
+}
+
+// td_reserve's workspace-placement probe (td_api.cpp place_ws): the same code as
+// turbo_decode_kernel under its own symbol, so that kernel traces and PMC passes of a decode list
+// the one-iteration probe launches apart from the decode's own launches.
+template <typename T, int ALGO>
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_placement_probe_kernel(
+    DecodeParams<T> p)
+{
+    turbo_decode_body<T, ALGO>(p);
 }
 
 // Standalone SISO (Log_MAP_decoder) over interleaved [G][L][8] inputs.
@@ -1950,8 +1966,11 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
     for (int j = 0; j < 8; ++j) v[j] = (j == 0 || !slot0_only) ? x0 : (T)-kInfty;
 }
 
+#ifndef TD_SW_WAVES
+#define TD_SW_WAVES 1   // minimum waves per SIMD asked of the register allocator (1: no limit)
+#endif
 template <typename T, int ALGO, int S>
-__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
+__global__ __launch_bounds__(256, TD_SW_WAVES) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[kLutElems<T>];
     if constexpr (ALGO == 0) {
@@ -2291,12 +2310,18 @@ constexpr size_t wg_lds()
 static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
 
 template <typename T, int ALGO>
-hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st)
+hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool probe)
 {
-    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>), wg_lds<T>());
+    const void* k = probe ? reinterpret_cast<const void*>(&turbo_placement_probe_kernel<T, ALGO>)
+                          : reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>);
+    hipError_t e = allow_smem(k, wg_lds<T>());
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
-                       wg_lds<T>(), st, p);
+    if (probe)
+        hipLaunchKernelGGL((turbo_placement_probe_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg),
+                           dim3(kGroupsPerWg * kWaves * kLanes), wg_lds<T>(), st, p);
+    else
+        hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg),
+                           dim3(kGroupsPerWg * kWaves * kLanes), wg_lds<T>(), st, p);
     return hipGetLastError();
 }
 
@@ -2327,9 +2352,9 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 }
 
 template <typename T>
-hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st)
+hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st, bool probe)
 {
-    return p.algo == 1 ? launch_turbo_algo<T, 1>(p, st) : launch_turbo_algo<T, 0>(p, st);
+    return p.algo == 1 ? launch_turbo_algo<T, 1>(p, st, probe) : launch_turbo_algo<T, 0>(p, st, probe);
 }
 
 template <typename T>
@@ -2349,12 +2374,12 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
-template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t);
+template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t, bool);
 template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, const WindowBufs<double>&,
                                          hipStream_t);
 template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, const WindowBufs<float>&,
                                         hipStream_t);
-template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t);
+template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t, bool);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);
 template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*, const float*, float*, int, float*,
