@@ -67,7 +67,7 @@ int td_reserve(td_handle* h, int B);
 /* td_reserve of the exact schedule for B >= 1024 also picks the workspace's placement: the turbo
  * kernel's speed depends on the physical pages behind it (two modes 6-7 % apart on MI355X), so it
  * times one iteration on candidate workspaces (up to TD_PLACEMENT_TRIALS, environment variable,
- * default 10; 1 = a plain allocation; stopping once both modes were seen) and keeps the fastest.
+ * default 24; 1 = a plain allocation; stopping once both modes were seen) and keeps the fastest.
  * Results do not depend on it. */
 
 /*

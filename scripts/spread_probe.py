@@ -36,5 +36,7 @@ for i in range(ninst):
         _, turbo_ms, _n = codec.kernel_ms()
         codec.profile(False)
         row.append("%.2f/%.0f" % (turbo_ms, B * K * steps / dt / 1e6))
-    print("instance", i, "kernel_ms/Mbps per batch:", " ".join(row), "placement", codec.placement(), flush=True)
+    errs = int((bits.cpu().numpy() != u).sum())
+    print("instance", i, "kernel_ms/Mbps per batch:", " ".join(row), "placement", codec.placement(), "bit errors", errs,
+          flush=True)
     keep.append(codec)   # keep the workspace so the next instance gets another allocation

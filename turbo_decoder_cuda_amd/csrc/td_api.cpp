@@ -158,7 +158,7 @@ Carve carve(int G, int K, size_t elem)
     const int L = K + td::kMemory;
     const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
     const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
-    const size_t arrA = align_up(((size_t)G * L + td::window_steps()) * 64 * elem, 256);   // + one window: DMA tail
+    const size_t arrA = align_up(((size_t)G * td::astore_group_elems(L) + (size_t)td::window_steps() * 64) * elem, 256);   // + one window: DMA tail
     Carve c{};
     c.sys1 = 0;
     c.par1 = c.sys1 + arrL;
@@ -211,7 +211,7 @@ int ensure_ws(td_handle* h, int G)
 // candidates, all held until the choice (so each one gets fresh pages), times one turbo iteration
 // on each (best of two launches; zeroed workspace, results discarded; 2.20 vs 2.32 ms in the two modes at config 2) and
 // keeps the fastest.  It stops once two candidates differ by more than 4 % (both modes seen), at
-// TD_PLACEMENT_TRIALS candidates (environment, default 10; 1 = a plain allocation), or when the
+// TD_PLACEMENT_TRIALS candidates (environment, default 24; 1 = a plain allocation), or when the
 // next one would take the held candidates past half the free device memory.  Results never depend
 // on the placement.
 template <typename T>
@@ -255,7 +255,7 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
 
 int place_ws(td_handle* h, int G)
 {
-    int trials = 10;
+    int trials = 24;
     if (const char* e = std::getenv("TD_PLACEMENT_TRIALS")) trials = std::atoi(e);
     if (G <= h->ws_groups || trials <= 1 || h->wp.window || 8 * G < 1024) return ensure_ws(h, G);
     if (h->d_ws) {
@@ -447,7 +447,7 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     const int W = td::window_steps();
     const int nT = (L + W - 1) / W;
     const size_t eL = (size_t)G * L * 8 * sizeof(T);
-    const size_t eA = ((size_t)G * L + td::window_steps()) * 64 * sizeof(T);
+    const size_t eA = ((size_t)G * td::astore_group_elems(L) + (size_t)td::window_steps() * 64) * sizeof(T);
     const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
     char* buf = nullptr;
     // zero permutation tables (the bare SISO writes no extrinsic), with the loader's spare ints

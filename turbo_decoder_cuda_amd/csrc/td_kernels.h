@@ -31,6 +31,13 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 // group g = codewords 8g..8g+7, element [g][step][c].
 constexpr int kPermPad = 16;         // spare ints after pi / pinv: the loader stages window-sized chunks
 constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
+// alpha scratch (astore) of one codeword group: L rows of 64 (8 codewords x 8 states) plus a pad of
+// TD_APAD elements between the groups' streams (a knob: pads of 512 B, 4 KiB and 32.5 KiB left the
+// placement modes of DESIGN.md 3.2 as they were)
+#ifndef TD_APAD
+#define TD_APAD 0
+#endif
+constexpr size_t astore_group_elems(int L) { return (size_t)L * 64 + TD_APAD; }
 
 template <typename T>
 struct DecodeParams {

@@ -585,7 +585,7 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
 {
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
-    const char* src = reinterpret_cast<const char*>(astore + ((size_t)gm.g * gm.L + (size_t)tc * kW) * kLanes);
+    const char* src = reinterpret_cast<const char*>(astore + (size_t)gm.g * astore_group_elems(gm.L) + (size_t)tc * kW * kLanes);
     const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
@@ -1319,7 +1319,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     const int nT = gm.nT;
     const int tl = nT - 1;
     const int nB = nT + 2;   // B-pass iterations: j = 0 .. nT+1 (wa = tl - j, wb = wa + 1, wf = wa + 2)
-    T* ga0 = astore + (size_t)gm.g * gm.L * kLanes;
+    T* ga0 = astore + (size_t)gm.g * astore_group_elems(gm.L);
     T* gtm0 = tmstore + (size_t)gm.g * gm.L * kCw;
 
     // ===================================== F pass
