@@ -15,6 +15,10 @@
 #include <vector>
 
 #include "td_kernels.h"
+
+#ifndef TD_SYS2_IN_TURBO
+#define TD_SYS2_IN_TURBO 1   // exact schedule: sys2 = sys1 o pi formed inside the turbo kernel (no demux_perm launch)
+#endif
 #include "td_tables.h"
 #include "turbo_mi355x.h"
 
@@ -236,6 +240,7 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
     dp.G = G;
     dp.B = 8 * G;
     dp.iters = 1;
+    dp.sys2_in_turbo = TD_SYS2_IN_TURBO;
     if (hipMemsetAsync(ws, 0, c.total, st) != hipSuccess) return -1.f;
     // untimed launches first (the first probe of a process also brings the clocks up), then the
     // best of two timed ones
@@ -405,6 +410,7 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.B = B;
     dp.iters = h->p.iterations;
     dp.all_iters = all_iters ? 1 : 0;
+    dp.sys2_in_turbo = (TD_SYS2_IN_TURBO && !h->wp.window) ? 1 : 0;
     td::WindowBufs<T> wb{};
     if (h->wp.window) {   // sized before anything is enqueued (a growth synchronises the device)
         rc = window_bufs<T>(h, dp, wb);

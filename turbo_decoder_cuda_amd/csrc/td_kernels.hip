@@ -362,6 +362,7 @@ struct SisoDst {
     int bits_stride;
     int dump_slot;
     int dump_stride;
+    T* sys2_out;      // first SISO only (sys2_in_turbo): sys2[g][i][c] = sys[g][pi[i]][c], i < K
 };
 
 struct Geom {
@@ -1485,6 +1486,38 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
+    } else if (dst.sys2_out) {
+        // waves 1 and 3, first SISO: SISO2's systematic input sys2[g][i][c] = sys1[g][pi(i)][c]
+        // (i < K; :1109-1113), one element of window t per lane (96 of 128 lanes) with pi(i) from
+        // the ring slot of window t (Wp[.][k][c][1], staged by the loader), loaded in iteration t
+        // and stored in t+1, so no wave ever waits on HBM before a barrier.  This is
+        // demux_perm_kernel's work, done by the waves the F pass leaves idle.
+        wg_sync_lds();
+        TD_STAMP(p1);
+        TD_ACC(11, p0, p1);
+        const int e = (wave == 1 ? 0 : kLanes) + lane;
+        const int ec = min(e, kTile - 1);
+        const int k = ec >> 3, c = ec & 7;
+        const T* s1 = src.sys + (size_t)gm.g * gm.L * kCw + c;
+        T* s2 = dst.sys2_out + (size_t)gm.g * gm.L * kCw + c;
+        T v = (T)0;
+        int ip = -1;   // row of the pending store
+        for (int t = 0; t < nT; ++t) {
+            TD_STAMP(f0);
+            const int pi_i = min(max(sm.Wp[t % 3][k][c][1], 0), gm.K - 1);   // spare rows past K: any valid row
+            const T nv = s1[(size_t)pi_i * kCw];
+            if (ip >= 0) s2[(size_t)ip * kCw] = v;
+            const int i = t * kW + k;
+            ip = (e < kTile && i < gm.K) ? i : -1;
+            v = nv;
+            TD_STAMP(f1);
+            wg_sync_lds();
+            TD_STAMP(f2);
+            TD_ACC(0, f0, f1);
+            TD_ACC(1, f1, f2);
+        }
+        if (ip >= 0) s2[(size_t)ip * kCw] = v;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // sys2 complete before the SISO's end barrier
     } else {
         wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
         TD_STAMP(p1);
@@ -1777,7 +1810,7 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
                        (dec == 0 && it == 0) ? 0 : p.K, 1};
         SisoDst<T> dst{dec ? p.ext21 : p.ext12, dec ? 2 : 3, p.K, nullptr, p.le_dump,
                        want_bits ? p.bits : nullptr, p.all_iters ? it : 0, p.all_iters ? p.iters * p.K : p.K,
-                       s, p.iters * 2 * p.L};
+                       s, p.iters * 2 * p.L, (s == 0 && p.sys2_in_turbo) ? p.sys2 : nullptr};
         TD_STAMP(s0);
         siso_wg<T, ALGO>(sm, src, dst, gm, p.astore, p.tmstore, p.lane, wave, lane, st);
         TD_STAMP(s1);
@@ -1827,7 +1860,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     __syncthreads();
     Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
-    SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0};
+    SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0, nullptr};
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
     wg_release(w, p.cu_slots);
 }
@@ -2344,7 +2377,7 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
     hipLaunchKernelGGL(demux_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, flow);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (!kDemuxPerm) return hipSuccess;
+    if (!kDemuxPerm || p.sys2_in_turbo) return hipSuccess;
     const int bpg = (p.K * kCw + kPermBlock - 1) / kPermBlock;
     const long long pblocks = (long long)((p.G + 7) / 8) * 8 * bpg;
     hipLaunchKernelGGL(demux_perm_kernel<T>, dim3((unsigned)pblocks), dim3(kPermBlock), 0, st, p, bpg);
