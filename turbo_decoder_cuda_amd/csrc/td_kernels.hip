@@ -884,6 +884,9 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
+#ifdef TD_DIAG_SPARSE_ASCHED   // diagnostics only (wrong log-MAP results): alpha stored at phase 0 only
+            if constexpr (PH == 0)
+#endif
             gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
@@ -1299,6 +1302,9 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #define TD_STAMP(v)
 #define TD_ACC(slot, a, b)
 #endif
+#ifndef TD_ALPHA_PRIO
+#define TD_ALPHA_PRIO 2   // VALU priority of the alpha wave in the F pass
+#endif
 constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
                                  // barriers, F prologue, loader B prologue, loader first tile (see diag)
@@ -1329,7 +1335,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
         T a = lc.a_init0 ? (T)0 : (T)-kInfty;   // alpha[.][0] (:943,948), its tempmax is 0
-        __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(TD_ALPHA_PRIO);
         wg_sync_lds();
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
