@@ -40,7 +40,7 @@ r = rec["K6144_B4096_it8_f64_logmap"]
 r.update(fetch_size_kib_raw=fk, write_size_kib_raw=wk, fetch_bytes=int(fk * 1024 * 2), write_bytes=int(wk * 1024),
          launches=len(f), kernel=f"{tag} ({desc})",
          source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) --kernel-trace of bench.py "
-                f"--steps 3 --warmup 1; profiles/{rnd}/{tag}_pmc_*.csv")
+                f"--steps 8 --warmup 1; profiles/{rnd}/{tag}_pmc_*.csv")
 r["bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
 json.dump(rec, open(path, "w"), indent=1)
 print(json.dumps(r, indent=1))

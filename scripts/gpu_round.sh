@@ -17,7 +17,7 @@ cat gpurun_out/smoke.log
 step bench
 timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed rc=$?"; tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
-PB="--steps 3 --warmup 1 --cpu-sample 0 --no-variants"
+PB="--steps 8 --warmup 1 --cpu-sample 0 --no-variants"
 step kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o kt --output-format csv -- python3 bench.py $PB > gpurun_out/prof_kt.log 2>&1 || { echo "rocprof kt failed rc=$?"; tail -20 gpurun_out/prof_kt.log; exit 1; }
 step pmc-fetch
