@@ -35,6 +35,17 @@ def test_header_and_exports_agree():
         assert hasattr(L, s), f"libturbo_mi355x.so does not export {s}"
 
 
+def test_placement_probe_has_its_own_kernel_symbol():
+    """td_reserve's one-iteration placement probes launch turbo_placement_probe_kernel, not
+    turbo_decode_kernel, so kernel traces and PMC passes of a decode average the decode's own
+    launches only (workspace placement).  Both names are in the gfx950 code object."""
+    blob = open(N.LIB_PATH, "rb").read()
+    for algo in (b"0", b"1"):
+        for t in (b"d", b"f"):
+            assert b"turbo_decode_kernelI" + t + b"Li" + algo in blob
+            assert b"turbo_placement_probe_kernelI" + t + b"Li" + algo in blob
+
+
 def test_abi_version_and_device_count():
     L = N.lib()
     assert L.td_abi_version() == 1
