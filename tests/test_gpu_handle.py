@@ -1,0 +1,85 @@
+"""Handle-level behaviour on the GPU: the workspace placement search of td_reserve and decodes
+captured into a hipGraph, both checked against the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    return torch.device("cuda", 0)
+
+
+def test_reserve_placement_search_decodes_like_the_oracle(monkeypatch):
+    """td_reserve with TD_PLACEMENT_TRIALS=3 at B=1024 (the smallest batch it searches at): 1 to
+    3 candidates timed, a valid pick, and a decode on the chosen workspace equal to the oracle."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    monkeypatch.setenv("TD_PLACEMENT_TRIALS", "3")
+    K, f1, f2, iters, B = 40, 3, 10, 3, 1024
+    _, flow = O.synth_batch(K, f1, f2, 0.5, 4242, B)
+    x = torch.from_numpy(flow).to(_dev())
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.reserve(B)
+        ms, pick = c.placement()
+        assert 1 <= len(ms) <= 3 and 0 <= pick < len(ms)
+        assert all(m > 0 for m in ms) and ms[pick] == min(ms)
+        bits = c.decode(x)
+        torch.cuda.synchronize()
+    ob = O.decode_batch(np.ascontiguousarray(flow), K, f1, f2, iters, nthreads=8)
+    assert np.array_equal(bits.cpu().numpy(), ob)
+
+
+def test_plain_allocation_reports_no_placement(monkeypatch):
+    from turbo_decoder_cuda_amd import TurboCodec
+    monkeypatch.setenv("TD_PLACEMENT_TRIALS", "1")
+    with TurboCodec(40, 3, 10, iterations=2) as c:
+        c.reserve(2048)
+        assert c.placement() == ([], -1)
+
+
+def test_graph_capture_between_eager_decodes():
+    """Eager decode on stream A, capture of a decode on stream B (torch.cuda.graph, hipGraph
+    capture), two replays, then an eager decode on stream C: every output equals the oracle.  The
+    captured decode neither waits on nor records the handle's workspace event (td_api.cpp), so
+    the capture stays isolated and the later eager decode does not wait on a captured event."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2, iters, B = 1024, 31, 64, 3, 16
+    dev = _dev()
+    flows = [O.synth_batch(K, f1, f2, 0.2 + 0.1 * k, 500 + k, B)[1] for k in range(3)]
+    ref = [O.decode_batch(np.ascontiguousarray(f), K, f1, f2, iters, nthreads=8) for f in flows]
+    xs = [torch.from_numpy(f).to(dev) for f in flows]
+    sa, sb, sc = (torch.cuda.Stream(dev) for _ in range(3))
+    torch.cuda.synchronize()
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.reserve(B)   # no workspace growth inside the capture
+        with torch.cuda.stream(sa):
+            out_a = c.decode(xs[0], stream=sa)
+        sa.synchronize()
+        assert np.array_equal(out_a.cpu().numpy(), ref[0])
+
+        gin = xs[1].clone()
+        gout = torch.empty((B, K), dtype=torch.uint8, device=dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=sb):
+            c.decode(gin, gout, stream=sb)
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(gout.cpu().numpy(), ref[1])
+        gin.copy_(xs[2])
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(gout.cpu().numpy(), ref[2])
+
+        with torch.cuda.stream(sc):
+            out_c = c.decode(xs[0], stream=sc)
+        sc.synchronize()
+        assert np.array_equal(out_c.cpu().numpy(), ref[0])

@@ -19,6 +19,9 @@
 #ifndef TD_SYS2_IN_TURBO
 #define TD_SYS2_IN_TURBO 1   // exact schedule: sys2 = sys1 o pi formed inside the turbo kernel (no demux_perm launch)
 #endif
+#ifndef TD_PLACEMENT_DEFAULT
+#define TD_PLACEMENT_DEFAULT 24   // td_reserve's workspace candidates (TD_PLACEMENT_TRIALS overrides)
+#endif
 #include "td_tables.h"
 #include "turbo_mi355x.h"
 
@@ -88,6 +91,9 @@ struct td_handle {
     hipEvent_t ws_free = nullptr;   // recorded after the last decode's kernels
     hipStream_t ws_stream = nullptr;
     bool ws_pending = false;
+#ifdef TD_WS_EXPERIMENT
+    char* ovr[8] = {};   // diagnostics: workspace arrays taken from another handle (td_debug_swap_arrays)
+#endif
 };
 
 namespace td {
@@ -162,7 +168,7 @@ Carve carve(int G, int K, size_t elem)
     const int L = K + td::kMemory;
     const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
     const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
-    const size_t arrA = align_up(((size_t)G * td::astore_group_elems(L) + (size_t)td::window_steps() * 64) * elem, 256);   // + one window: DMA tail
+    const size_t arrA = align_up(td::astore_elems(G, L) * elem, 256);
     Carve c{};
     c.sys1 = 0;
     c.par1 = c.sys1 + arrL;
@@ -181,13 +187,80 @@ Carve carve(int G, int K, size_t elem)
     return c;
 }
 
+// Workspace allocations.  TD_WS_VMM builds (diagnostics) map the workspace through the virtual
+// memory API instead: physical chunks of TD_VMM_CHUNK bytes (environment; 0 = one chunk) from
+// hipMemCreate, mapped into one reserved range -- to see whether the placement modes follow the
+// page / fragment size behind the workspace.
+#ifdef TD_WS_VMM
+struct VmmRec {
+    void* ptr;
+    size_t size;
+    std::vector<hipMemGenericAllocationHandle_t> chunks;
+};
+std::vector<VmmRec> g_vmm;
+hipError_t ws_malloc(void** p, size_t size)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e != hipSuccess) return e;
+    size_t chunk = 0;
+    if (const char* c = std::getenv("TD_VMM_CHUNK")) chunk = std::strtoull(c, nullptr, 0);
+    size = align_up(size, gran);
+    chunk = chunk ? align_up(chunk, gran) : size;
+    VmmRec r{nullptr, size, {}};
+    e = hipMemAddressReserve(&r.ptr, size, std::max(gran, (size_t)2 << 20), nullptr, 0);
+    if (e != hipSuccess) return e;
+    for (size_t o = 0; o < size; o += chunk) {
+        const size_t n = std::min(chunk, size - o);
+        hipMemGenericAllocationHandle_t hd;
+        e = hipMemCreate(&hd, n, &prop, 0);
+        if (e != hipSuccess) return e;
+        r.chunks.push_back(hd);
+        e = hipMemMap(static_cast<char*>(r.ptr) + o, n, 0, hd, 0);
+        if (e != hipSuccess) return e;
+    }
+    hipMemAccessDesc acc{};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(r.ptr, size, &acc, 1);
+    if (e != hipSuccess) return e;
+    std::fprintf(stderr, "td: VMM workspace %zu B in %zu chunk(s), granularity %zu\n", size, r.chunks.size(), gran);
+    *p = r.ptr;
+    g_vmm.push_back(std::move(r));
+    return hipSuccess;
+}
+hipError_t ws_release(void* p)
+{
+    for (size_t i = 0; i < g_vmm.size(); ++i)
+        if (g_vmm[i].ptr == p) {
+            (void)hipDeviceSynchronize();
+            (void)hipMemUnmap(p, g_vmm[i].size);
+            for (auto hd : g_vmm[i].chunks) (void)hipMemRelease(hd);
+            (void)hipMemAddressFree(p, g_vmm[i].size);
+            g_vmm.erase(g_vmm.begin() + i);
+            return hipSuccess;
+        }
+    return hipFree(p);
+}
+#else
+hipError_t ws_malloc(void** p, size_t size) { return hipMalloc(p, size); }
+hipError_t ws_release(void* p) { return hipFree(p); }
+#endif
+
 int ensure_ws(td_handle* h, int G)
 {
     if (G <= h->ws_groups) return TD_OK;
     const Carve c = carve(G, h->p.K, h->elem);
     if (h->d_ws) {
         TD_HIP(hipDeviceSynchronize());
-        TD_HIP(hipFree(h->d_ws));
+        TD_HIP(ws_release(h->d_ws));
         h->d_ws = nullptr;
         h->ws_groups = 0;
     }
@@ -196,7 +269,7 @@ int ensure_ws(td_handle* h, int G)
 #elif defined(TD_WS_EXPERIMENT)
     if (hipMalloc(&h->d_ws, c.total + (512u << 20)) != hipSuccess) {
 #else
-    if (hipMalloc(&h->d_ws, c.total) != hipSuccess) {
+    if (ws_malloc(&h->d_ws, c.total) != hipSuccess) {
 #endif
         h->d_ws = nullptr;
         return fail(TD_ENOMEM, "hipMalloc of the decode workspace failed (" + std::to_string(c.total) + " B)");
@@ -258,58 +331,83 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
     return best;
 }
 
+// Stop rule of the placement search: the fast mode has been seen once some candidate runs >= 4 %
+// below the median of all candidates probed so far (at least three, so that the median is a mode and
+// not an average of the two).  A slow straggler never stops the search: with every candidate in
+// the slow mode the median is slow too and nothing is 4 % below it.  (Until round 3 the rule was
+// "two candidates differ by 4 %", which an upward outlier among slow candidates satisfied.)
+bool placement_fast_seen(const std::vector<float>& ms)
+{
+    std::vector<float> v;
+    for (float x : ms)
+        if (x > 0 && x < 1e29f) v.push_back(x);
+    if (v.size() < 3) return false;
+    std::sort(v.begin(), v.end());
+    const float med = v.size() % 2 ? v[v.size() / 2] : 0.5f * (v[v.size() / 2 - 1] + v[v.size() / 2]);
+    return v.front() < 0.96f * med;
+}
+
+// Candidate workspaces the search may hold at once: half the free device memory, and at most
+// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.
+constexpr size_t kPlaceHoldBytes = (size_t)48 << 30;
+
 int place_ws(td_handle* h, int G)
 {
-    int trials = 24;
+    int trials = TD_PLACEMENT_DEFAULT;
     if (const char* e = std::getenv("TD_PLACEMENT_TRIALS")) trials = std::atoi(e);
     if (G <= h->ws_groups || trials <= 1 || h->wp.window || 8 * G < 1024) return ensure_ws(h, G);
     if (h->d_ws) {
         TD_HIP(hipDeviceSynchronize());
-        TD_HIP(hipFree(h->d_ws));
+        TD_HIP(ws_release(h->d_ws));
         h->d_ws = nullptr;
         h->ws_groups = 0;
     }
     const Carve c = carve(G, h->p.K, h->elem);
-    hipStream_t st = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    TD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    TD_HIP(hipEventCreate(&e0));
-    TD_HIP(hipEventCreate(&e1));
+    // every HIP object of the search is released on every exit path, error returns included
+    struct Search {
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        std::vector<std::pair<float, void*>> cand;
+        ~Search()
+        {
+            if (st) (void)hipStreamSynchronize(st);
+            for (auto& x : cand)
+                if (x.second) (void)ws_release(x.second);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            if (st) (void)hipStreamDestroy(st);
+        }
+    } s;
+    TD_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+    TD_HIP(hipEventCreate(&s.e0));
+    TD_HIP(hipEventCreate(&s.e1));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    std::vector<std::pair<float, void*>> cand;
-    float lo = 1e30f, hi = 0.f;
+    const size_t hold = std::min(free_b / 2, kPlaceHoldBytes);
+    std::vector<float> ms_all;
     for (int i = 0; i < trials; ++i) {
-        if (i > 0 && (size_t)(i + 1) * c.total > free_b / 2) break;   // memory guard
+        if (i > 0 && (size_t)(i + 1) * c.total > hold) break;   // memory guard
         void* p = nullptr;
-        if (hipMalloc(&p, c.total) != hipSuccess) break;   // out of memory: choose among those we have
+        if (ws_malloc(&p, c.total) != hipSuccess) break;   // out of memory: choose among those we have
+        s.cand.emplace_back(1e30f, p);
         const int warm = i == 0 ? 4 : 1;
-        const float ms = h->elem == 8 ? probe_ws<double>(h, static_cast<char*>(p), G, st, e0, e1, warm)
-                                      : probe_ws<float>(h, static_cast<char*>(p), G, st, e0, e1, warm);
-        cand.emplace_back(ms < 0 ? 1e30f : ms, p);
-        if (ms > 0) {
-            lo = std::min(lo, ms);
-            hi = std::max(hi, ms);
-        }
-        if (cand.size() >= 2 && lo < 0.96f * hi) break;   // both modes seen: the fast one is among them
+        const float ms = h->elem == 8 ? probe_ws<double>(h, static_cast<char*>(p), G, s.st, s.e0, s.e1, warm)
+                                      : probe_ws<float>(h, static_cast<char*>(p), G, s.st, s.e0, s.e1, warm);
+        s.cand.back().first = ms < 0 ? 1e30f : ms;
+        ms_all.push_back(s.cand.back().first);
+        if (placement_fast_seen(ms_all)) break;
     }
     (void)hipGetLastError();
-    (void)hipStreamSynchronize(st);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipStreamDestroy(st);
-    if (cand.empty()) return ensure_ws(h, G);
+    if (s.cand.empty()) return ensure_ws(h, G);
     size_t best = 0;
-    for (size_t i = 1; i < cand.size(); ++i)
-        if (cand[i].first < cand[best].first) best = i;
-    for (size_t i = 0; i < cand.size(); ++i)
-        if (i != best) TD_HIP(hipFree(cand[i].second));
-    h->d_ws = cand[best].second;
+    for (size_t i = 1; i < s.cand.size(); ++i)
+        if (s.cand[i].first < s.cand[best].first) best = i;
+    h->place_ms = ms_all;
+    h->place_pick = (int)best;
+    h->d_ws = s.cand[best].second;
+    s.cand[best].second = nullptr;   // kept; the guard frees the others
     h->ws_bytes = c.total;
     h->ws_groups = G;
-    h->place_ms.clear();
-    for (auto& x : cand) h->place_ms.push_back(x.first);
-    h->place_pick = (int)best;
     return TD_OK;
 }
 
@@ -397,6 +495,13 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.ext21 = reinterpret_cast<T*>(ws + c.ext21);
     dp.astore = reinterpret_cast<T*>(ws + c.astore);
     dp.tmstore = reinterpret_cast<T*>(ws + c.tmstore);
+#ifdef TD_WS_EXPERIMENT
+    {
+        T** arr[8] = {&dp.sys1, &dp.par1, &dp.sys2, &dp.par2, &dp.ext12, &dp.ext21, &dp.astore, &dp.tmstore};
+        for (int i = 0; i < 8; ++i)
+            if (h->ovr[i]) *arr[i] = reinterpret_cast<T*>(h->ovr[i]);
+    }
+#endif
     dp.llr_out = nullptr;
     dp.pi = h->d_pi;
     dp.pinv = h->d_pinv;
@@ -416,10 +521,19 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
         rc = window_bufs<T>(h, dp, wb);
         if (rc) return rc;
     }
-    if (!h->ws_free) TD_HIP(hipEventCreateWithFlags(&h->ws_free, hipEventDisableTiming));
-    if (h->ws_pending && st != h->ws_stream) TD_HIP(hipStreamWaitEvent(st, h->ws_free, 0));
+    // A decode captured into a hipGraph neither waits on nor records the workspace event: an event
+    // recorded outside the capture would break its isolation, and one recorded inside it could not
+    // be waited on by a later eager decode.  Replays are therefore not ordered against eager
+    // decodes on the same handle (the caller orders them, e.g. on one stream).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    TD_HIP(hipStreamIsCapturing(st, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (!capturing) {
+        if (!h->ws_free) TD_HIP(hipEventCreateWithFlags(&h->ws_free, hipEventDisableTiming));
+        if (h->ws_pending && st != h->ws_stream) TD_HIP(hipStreamWaitEvent(st, h->ws_free, 0));
+    }
     hipEvent_t* ev = nullptr;
-    if (h->prof) {
+    if (h->prof && !capturing) {
         if (h->nev == h->ev.size()) {
             std::array<hipEvent_t, 3> tri{};
             for (auto& x : tri) TD_HIP(hipEventCreate(&x));
@@ -440,9 +554,11 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
         TD_HIP(hipEventRecord(ev[2], st));
         ++h->nev;
     }
-    TD_HIP(hipEventRecord(h->ws_free, st));
-    h->ws_stream = st;
-    h->ws_pending = true;
+    if (!capturing) {
+        TD_HIP(hipEventRecord(h->ws_free, st));
+        h->ws_stream = st;
+        h->ws_pending = true;
+    }
     return TD_OK;
 }
 
@@ -453,7 +569,7 @@ int siso_host_t(td_handle* h, const void* recs, const void* La, int terminated, 
     const int W = td::window_steps();
     const int nT = (L + W - 1) / W;
     const size_t eL = (size_t)G * L * 8 * sizeof(T);
-    const size_t eA = ((size_t)G * td::astore_group_elems(L) + (size_t)td::window_steps() * 64) * sizeof(T);
+    const size_t eA = td::astore_elems(G, L) * sizeof(T);
     const size_t inR = (size_t)B * 2 * L * sizeof(T), inA = (size_t)B * L * sizeof(T);
     char* buf = nullptr;
     // zero permutation tables (the bare SISO writes no extrinsic), with the loader's spare ints
@@ -700,7 +816,7 @@ int td_destroy(td_handle* h)
 {
     if (!h) return TD_OK;
     (void)hipSetDevice(h->p.device);
-    if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->d_ws) (void)ws_release(h->d_ws);
     if (h->d_pi) (void)hipFree(h->d_pi);
     if (h->d_pinv) (void)hipFree(h->d_pinv);
     if (h->d_lut) (void)hipFree(h->d_lut);
@@ -794,6 +910,38 @@ int td_debug_placement(td_handle* h, float* ms, int cap, int* pick)
     if (pick) *pick = h->place_pick;
     return n;
 }
+
+#ifdef TD_WS_EXPERIMENT
+// Diagnostics build only (not in the header): swap workspace arrays between two handles of the same
+// K, precision and reserved batch, to find which array carries the placement mode.
+// mask bits 0-7: sys1 par1 sys2 par2 ext12 ext21 astore tmstore; bit 8: pi + pinv; bit 9: the
+// max* table, lane tables and CU slot words.  Swapping twice restores both handles.
+int td_debug_swap_arrays(td_handle* a, td_handle* b, int mask)
+{
+    if (!a || !b || a->p.K != b->p.K || a->elem != b->elem || a->ws_groups != b->ws_groups || !a->d_ws || !b->d_ws)
+        return fail(TD_EINVAL, "td_debug_swap_arrays: handles differ");
+    TD_HIP(hipDeviceSynchronize());
+    const Carve c = carve(a->ws_groups, a->p.K, a->elem);
+    const size_t off[8] = {c.sys1, c.par1, c.sys2, c.par2, c.ext12, c.ext21, c.astore, c.tmstore};
+    for (int i = 0; i < 8; ++i)
+        if ((mask >> i) & 1) {
+            char* ea = a->ovr[i] ? a->ovr[i] : static_cast<char*>(a->d_ws) + off[i];
+            char* eb = b->ovr[i] ? b->ovr[i] : static_cast<char*>(b->d_ws) + off[i];
+            a->ovr[i] = eb;
+            b->ovr[i] = ea;
+        }
+    if ((mask >> 8) & 1) {
+        std::swap(a->d_pi, b->d_pi);
+        std::swap(a->d_pinv, b->d_pinv);
+    }
+    if ((mask >> 9) & 1) {
+        std::swap(a->d_lut, b->d_lut);
+        std::swap(a->d_lane, b->d_lane);
+        std::swap(a->d_slots, b->d_slots);
+    }
+    return TD_OK;
+}
+#endif
 
 int td_debug_stamp_slots(void)
 {

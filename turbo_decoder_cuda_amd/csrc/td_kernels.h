@@ -38,6 +38,33 @@ constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
 #define TD_APAD 0
 #endif
 constexpr size_t astore_group_elems(int L) { return (size_t)L * 64 + TD_APAD; }
+// Alpha scratch layout (TD_AWIN, a knob): 0 (default) group-major [G][L][64] (+ TD_APAD per
+// group); 1 window-major [nT][G][kWindowSteps][64] (window t of every group one contiguous region);
+// 2 step-major [nT * kWindowSteps][G][64] (the row of step i of every group one 32 KiB span).
+// Measured in round 3 against the placement modes of DESIGN.md 3.2: all three keep the two modes
+// (fast 17.6-17.9 ms / slow 18.5-19.2 ms at config 2, plain allocations), and group-major has the
+// fastest fast mode, so it stays the default; td_reserve's placement search remains the remedy.
+#ifndef TD_AWIN
+#define TD_AWIN 0
+#endif
+constexpr int kWindowSteps = 12;   // td_kernels.hip kW
+constexpr int awin_windows(int L) { return (L + kWindowSteps - 1) / kWindowSteps; }
+constexpr size_t astore_elems(int G, int L)
+{
+    return TD_AWIN ? (size_t)awin_windows(L) * G * kWindowSteps * 64
+                   : (size_t)G * astore_group_elems(L) + (size_t)kWindowSteps * 64;   // + one window: DMA tail
+}
+// element offset of row 0 of window t of group g
+constexpr size_t astore_window_off(int g, int t, int G, int L)
+{
+    return TD_AWIN == 2 ? ((size_t)t * kWindowSteps * G + g) * 64
+         : TD_AWIN      ? ((size_t)t * G + g) * kWindowSteps * 64
+                        : (size_t)g * astore_group_elems(L) + (size_t)t * kWindowSteps * 64;
+}
+// distance between the first rows of windows t and t+1 of one group
+constexpr size_t astore_window_stride(int G) { return TD_AWIN ? (size_t)G * kWindowSteps * 64 : (size_t)kWindowSteps * 64; }
+// distance between consecutive rows (steps) of one group
+constexpr size_t astore_row_stride(int G) { return TD_AWIN == 2 ? (size_t)G * 64 : 64; }
 
 template <typename T>
 struct DecodeParams {
@@ -47,7 +74,7 @@ struct DecodeParams {
     T* par2;   // [G][L][8] parity 2
     T* ext12;  // [G][K][8] Le of decoder 1 scattered to interleaved order (= La of decoder 2)
     T* ext21;  // [G][K][8] Le of decoder 2 scattered to natural order (= La of decoder 1)
-    T* astore;    // [G][L][64] alpha[.][i] by 8c + state (F pass -> B pass scratch)
+    T* astore;    // alpha[.][i] by 8c + state (F pass -> B pass scratch), windows at astore_window_off
     T* tmstore;   // [G][L][8] tempmax[i+1] per step and codeword
     T* llr_out;                 // bare SISO: [G][L][8]
     const int* pi;              // [K] QPP

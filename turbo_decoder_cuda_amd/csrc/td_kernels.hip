@@ -366,7 +366,7 @@ struct SisoDst {
 };
 
 struct Geom {
-    int K, L, nT, B, g;
+    int K, L, nT, B, g, G;
     const int* pi;     // QPP pi[i]
     const int* pinv;   // its inverse
 };
@@ -447,6 +447,16 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(save)
                  : "s"(lds), "v"(src)
+                 : "memory");
+}
+
+// dma16 with a wave-uniform SGPR base and a per-lane 32-bit byte offset (saddr form)
+__device__ __forceinline__ void dma16_s(unsigned lds, const void* sbase, unsigned voff)
+{
+    unsigned save;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "s"(lds), "v"(voff), "s"(sbase)
                  : "memory");
 }
 
@@ -540,7 +550,8 @@ static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes")
 static_assert(kMemory + kW - 2 < kPermPad, "write-position chunks stay within the padded tables");
 
 // ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
-// Scratch layout: alpha [g][L][64] by 8c + state, tempmax [g][L][8].
+// Scratch layout: alpha by 8c + state in windows of kW rows (astore_window_off: window-major
+// [nT][G][kW][64] by default, td_kernels.h TD_AWIN), tempmax [g][L][8].
 // alpha of window t: HBM scratch -> LDS slot t % 3 directly (global_load_lds_dwordx4, no
 // registers): the window's kW rows are one contiguous 6 KiB block on both sides.  Completion is
 // tracked by vmcnt; the loader waits for it before the barrier that publishes the slot.
@@ -586,24 +597,30 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
 {
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
-    const char* src = reinterpret_cast<const char*>(astore + (size_t)gm.g * astore_group_elems(gm.L) + (size_t)tc * kW * kLanes);
+    const char* src = reinterpret_cast<const char*>(astore + astore_window_off(gm.g, tc, gm.G, gm.L));
     const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
+    // The window's rows are arow_bytes apart (step-major: G groups; else contiguous).  Each DMA
+    // covers rpd LDS rows; its first source row is a wave-uniform SGPR base, the lane's row and
+    // chunk within it a 32-bit offset (saddr form: no 64-bit per-lane addresses, 17 VGPRs fewer
+    // in the fp64 log-MAP kernel than per-lane pointers).  LDS row r holds the window's step r
+    // (max-log: ck_step(r)); chunk pc of codeword block cb holds the block's chunk
+    // (pc - av_rot) mod kBlkChunks (blk_off).
+    const unsigned arow_bytes = (unsigned)(astore_row_stride(gm.G) * sizeof(T));
+    constexpr int lpr = row_bytes / 16, rpd = kLanes / lpr;   // lanes per row, rows per DMA
 #pragma unroll
     for (int q = 0; q < n; ++q) {
-        // LDS byte b of the copied block: row r = b / row_bytes (log-MAP rows are the window's
-        // steps; max-log row r is step ck_step(r)), chunk pc of codeword block cb, which holds the
-        // block's chunk (pc - av_rot) mod kBlkChunks (blk_off)
-        const int b = q * kDmaBytes + lane * 16;
-        int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
+        const int r = q * rpd + lane / lpr, w = (lane % lpr) * 16;
+        int wo = w;
         if constexpr (kFoldSwz<T>) {
-            const int r = b / row_bytes, w = b % row_bytes;
             constexpr int blk = 8 * (int)sizeof(T);
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
-            off = (ALGO == 1 ? ck_step(r) : r) * row_bytes + (w / blk) * blk + pc * 16;
+            wo = (w / blk) * blk + pc * 16;
         }
-        dma16(lds + q * kDmaBytes, src + off);
+        const int s0 = ALGO == 1 ? ck_step(q * rpd) : q * rpd;   // source step of the DMA's first row
+        const int sr = ALGO == 1 ? ck_step(r) : r;
+        dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
     }
 }
 
@@ -781,7 +798,7 @@ struct AlphaSched {
     // alpha step K (phase K mod 3) of a full window: a = alpha_raw[.][i] in, alpha_raw[.][i+1] out;
     // op[K % 3] holds this step's operands, op[(K + 2) % 3] receives step K+2's
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
-                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0)
+                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0, size_t arow)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -799,17 +816,17 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        gstore(ga + K * kLanes + lc.st_off[PH], alpha);
+        gstore(ga + K * arow + lc.st_off[PH], alpha);
         gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
-        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0);
+        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0, arow);
     }
 };
 template <typename T>
 struct AlphaSched<T, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, T*)
+                                               const LaneConst<T>&, T*, T*, T*, size_t)
     {
     }
 };
@@ -861,11 +878,23 @@ __device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm, unsigned v
     }
 }
 
+// alpha row K of a full window: wave-uniform base sa in SGPRs, per-lane byte offset voff.  Window-
+// and group-major layouts (TD_AWIN 0, 1): sa = row 6 of the window and the row is an immediate offset
+// (no per-step address arithmetic); step-major (TD_AWIN 2): sa = row 0, rows arow elements apart.
+template <typename T, int K>
+__device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v, size_t arow)
+{
+    if constexpr (TD_AWIN == 2)
+        gstore_s<0>(sa + K * arow, voff, v);
+    else
+        gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, voff, v);
+}
+
 template <typename T, int ALGO, int K>
 struct AlphaSchedS {
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
                                                int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
-                                               unsigned vtm, TmBatch<T>& tbh)
+                                               unsigned vtm, TmBatch<T>& tbh, size_t arow)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -887,7 +916,7 @@ struct AlphaSchedS {
 #ifdef TD_DIAG_SPARSE_ASCHED   // diagnostics only (wrong log-MAP results): alpha stored at phase 0 only
             if constexpr (PH == 0)
 #endif
-            gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
+            astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
@@ -896,18 +925,19 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr ((kCkPhases >> PH) & 1) gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, va[PH], alpha);
+            if constexpr ((kCkPhases >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
         }
-        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh);
+        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh, arow);
     }
 };
 template <typename T, int ALGO>
 struct AlphaSchedS<T, ALGO, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned, TmBatch<T>&)
+                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned, TmBatch<T>&,
+                                               size_t)
     {
     }
 };
@@ -960,7 +990,7 @@ struct BetaSched<T, -1> {
 // stores tempmax[L] after the last window.
 template <typename T, int ALGO>
 __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, const T* lut, int c,
-                                          const LaneConst<T>& lc, T* ga, T* gtm,
+                                          const LaneConst<T>& lc, T* ga, T* gtm, size_t arow,
                                           unsigned long long* chain_st = nullptr)
 {
     (void)chain_st;
@@ -972,15 +1002,15 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
             op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
             op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
             TD_CHAIN_T0(c0);
-            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0));
+            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0), arow);
             TD_CHAIN_ACC(c0);
             return a;
         }
     }
 #endif
     T* pa0 = ga + lc.st_off[0];
-    T* pa1 = ga + kLanes + lc.st_off[1];
-    T* pa2 = ga + 2 * kLanes + lc.st_off[2];
+    T* pa1 = ga + arow + lc.st_off[1];
+    T* pa2 = ga + 2 * arow + lc.st_off[2];
     T* ptm = gtm + c - (t > 0 ? kCw : 0);
     int k = 0;
     StepIn<T> i0 = alpha_in<T, 0>(sm, tb, 0, c, lc);   // operands read one step group ahead
@@ -993,35 +1023,35 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
         for (; k + 3 <= n; k += 3) {
             const StepIn<T> c1 = i1, c2 = i2;
             const int kn = min(k + 3, kW - 3);
-            const StepHalf<T> h = alpha_issue<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+            const StepHalf<T> h = alpha_issue<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * arow, ptm);
             __builtin_amdgcn_sched_barrier(0);
             i0 = alpha_in<T, 0>(sm, tb, kn, c, lc);
             i1 = alpha_in<T, 1>(sm, tb, kn + 1, c, lc);
             i2 = alpha_in<T, 2>(sm, tb, kn + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
             a = step_done<T, ALGO>(h);
-            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * arow, gtm + c + k * kCw);
+            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * arow, gtm + c + (k + 1) * kCw);
             ptm = gtm + c + (k + 2) * kCw;
         }
     } else {
         for (; k + 3 <= n; k += 3) {
             const StepIn<T> c1 = alpha_in<T, 1>(sm, tb, k + 1, c, lc);
             const StepIn<T> c2 = alpha_in<T, 2>(sm, tb, k + 2, c, lc);
-            a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+            a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * arow, ptm);
             i0 = alpha_in<T, 0>(sm, tb, min(k + 3, kW - 1), c, lc);
-            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * kLanes, gtm + c + k * kCw);
-            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * kLanes, gtm + c + (k + 1) * kCw);
+            a = alpha_step<T, ALGO, 1>(a, c1, lut, lc, pa1 + k * arow, gtm + c + k * kCw);
+            a = alpha_step<T, ALGO, 2>(a, c2, lut, lc, pa2 + k * arow, gtm + c + (k + 1) * kCw);
             ptm = gtm + c + (k + 2) * kCw;
         }
         i1 = alpha_in<T, 1>(sm, tb, min(k + 1, kW - 1), c, lc);
     }
     if (k < n) {
-        a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * kLanes, ptm);
+        a = alpha_step<T, ALGO, 0>(a, i0, lut, lc, pa0 + k * arow, ptm);
         ptm = gtm + c + k * kCw;
     }
     if (k + 1 < n) {
-        a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * kLanes, ptm);
+        a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * arow, ptm);
     }
     return a;
 }
@@ -1326,7 +1356,13 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     const int nT = gm.nT;
     const int tl = nT - 1;
     const int nB = nT + 2;   // B-pass iterations: j = 0 .. nT+1 (wa = tl - j, wb = wa + 1, wf = wa + 2)
-    T* ga0 = astore + (size_t)gm.g * astore_group_elems(gm.L);
+    T* ga0 = astore + astore_window_off(gm.g, 0, gm.G, gm.L);   // row 0 of window 0 of this group
+    const size_t aws = astore_window_stride(gm.G);                // window t starts at ga0 + t * aws
+#if TD_AWIN == 2
+    const size_t arow = astore_row_stride(gm.G);                  // rows of a window, arow elements apart
+#else
+    constexpr size_t arow = kLanes;                               // rows of a window, arow elements apart
+#endif
     T* gtm0 = tmstore + (size_t)gm.g * gm.L * kCw;
 
     // ===================================== F pass
@@ -1343,10 +1379,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int t = 0; t < nT; t += 2) {
             TD_STAMP(f0);
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
+                                      ga0 + (size_t)t * aws, gtm0 + (size_t)t * kW * kCw, arow, st ? st + 4 : nullptr);
             if (t + 1 < nT)
                 a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                          ga0 + (size_t)(t + 1) * kW * kLanes, gtm0 + (size_t)(t + 1) * kW * kCw,
+                                          ga0 + (size_t)(t + 1) * aws, gtm0 + (size_t)(t + 1) * kW * kCw, arow,
                                           st ? st + 4 : nullptr);
 #else
         int t0 = 0;
@@ -1354,7 +1390,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             // windows 1 .. tl-1 are full: running bases and slot index, no per-window address math
             if (tl >= 2) {
                 TD_STAMP(f0);
-                a = alpha_window<T, ALGO>(a, 0, kW, sm, lut_col(sm, lane), c, lc, ga0, gtm0, st ? st + 4 : nullptr);
+                a = alpha_window<T, ALGO>(a, 0, kW, sm, lut_col(sm, lane), c, lc, ga0, gtm0, arow, st ? st + 4 : nullptr);
                 TD_STAMP(f1);
                 wg_sync_lds();
                 TD_STAMP(f2);
@@ -1365,7 +1401,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 const unsigned vtm = (unsigned)(c * sizeof(T));
                 TmBatch<T> tbh{(T)0, lane & 7, (unsigned)(((lane & 7) * kCw + c) * sizeof(T)),
                                (unsigned)(((lane & 3) * kCw + c) * sizeof(T))};
-                T* sa = ga0 + (size_t)(kW + 6) * kLanes;
+                T* sa = ga0 + aws + (TD_AWIN == 2 ? 0 : (size_t)6 * kLanes);   // window 1, row 6 (row 0: astore_row)
                 T* stm = gtm0 + (size_t)kW * kCw;
                 const T* lut = lut_col(sm, lane);
                 unsigned long long* chain_st = st ? st + 4 : nullptr;
@@ -1378,9 +1414,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
                     if (TD_AOP_FIRST) __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
                     TD_CHAIN_T0(c0);
-                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh);
+                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh, arow);
                     TD_CHAIN_ACC(c0);
-                    sa += (size_t)kW * kLanes;
+                    sa += aws;
                     stm += (size_t)kW * kCw;
                     tb = tb == 2 ? 0 : tb + 1;
                     TD_STAMP(f1);
@@ -1395,7 +1431,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int t = t0; t < nT; ++t) {
             TD_STAMP(f0);
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                      ga0 + (size_t)t * kW * kLanes, gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
+                                      ga0 + (size_t)t * aws, gtm0 + (size_t)t * kW * kCw, arow, st ? st + 4 : nullptr);
 #endif
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
@@ -1798,7 +1834,7 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
     if (wave == 1) set_beta_prio<T, ALGO>();   // beta first; alpha raises itself in the F pass
     __syncthreads();
 
-    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
+    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.G, p.pi, p.pinv};
     unsigned long long st[kStampSlots] = {};
 #ifdef TD_STAMPS
     const unsigned long long k_cyc0 = __builtin_amdgcn_s_memtime(), k_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1864,7 +1900,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
     lut_to_lds(p, sm, wave * kLanes + lane);
     if (wave == 1) set_beta_prio<T, ALGO>();
     __syncthreads();
-    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.pi, p.pinv};
+    Geom gm{p.K, p.L, p.nT, p.B, w.g, p.G, p.pi, p.pinv};
     SisoSrc<T> s{p.sys1, p.par1, la, p.L, p.L, terminated};
     SisoDst<T> d{nullptr, 0, 0, p.llr_out, nullptr, nullptr, 0, 0, 0, 0, nullptr};
     siso_wg<T, ALGO>(sm, s, d, gm, p.astore, p.tmstore, p.lane, wave, lane, nullptr);
@@ -2428,6 +2464,7 @@ template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*,
                                        hipStream_t);
 
 int window_steps() { return kW; }
+static_assert(kW == kWindowSteps, "td_kernels.h kWindowSteps is the kernel's window");
 int groups_per_wg() { return kGroupsPerWg; }
 
 }  // namespace td

@@ -69,12 +69,13 @@ class TurboCodec:
     def placement(self):
         """(probe ms of each candidate workspace, index kept) of the last reserve that allocated
         (td_debug_placement; ([], -1) for a plain allocation)."""
-        ms = (C.c_float * 16)()
         pick = C.c_int(-1)
-        n = N.lib().td_debug_placement(self._h, ms, 16, C.byref(pick))
+        n = N.lib().td_debug_placement(self._h, None, 0, C.byref(pick))   # the count first
         if n < 0:
             N.check(n)
-        return [round(ms[i], 4) for i in range(min(n, 16))], pick.value
+        ms = (C.c_float * max(n, 1))()
+        n = N.lib().td_debug_placement(self._h, ms, n, C.byref(pick))
+        return [round(ms[i], 4) for i in range(n)], pick.value
 
     def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
                    concurrent: bool = False) -> None:
