@@ -4,10 +4,15 @@
 
 Workload at N=1 = BASELINE config 2: batch 4096 x K=6144, 8 log-MAP (table max*) iterations,
 rate 1/3, fp64 parity arithmetic (the reference's precision and operation order).
-A "step" = one td_decode_device call on the resident batch (demultiplex + all iterations +
-hard decisions).  N>1: one process per GPU (torchrun), each decodes its own 4096-codeword
-shard -- weak scaling, no data-path collective; the only exchange is the max of the step
-times and the sum of error counters (gloo, host scalars).
+N>1 = BASELINE config 4: one process per GPU (torchrun), 32768 codewords per GPU (N=8: the
+262144-codeword batch; weak scaling), or with --strong the 262144 codewords split over the N
+ranks.  The global batch is ONE stream of frames, keyed by global codeword index: codeword j is
+frame j of ITTC/main.cpp's srand(seed) frame stream (td_synth_frames, bit-identical to the
+reference's frames), and rank r decodes its contiguous slice (shard_layout) -- so the ranks'
+bits concatenated are the single-process decode of the same global batch.  No data-path
+collective; the only exchange is the max of the step times and the sum of the error counters
+(gloo, host scalars).  A "step" = one td_decode_device call on the resident batch (demultiplex +
+all iterations + hard decisions).
 
 Extra objects on the JSON line:
   roofline      the turbo kernel against HBM (algorithmic bytes: fp64 LLR in + uint8 bits out
@@ -15,7 +20,8 @@ Extra objects on the JSON line:
                 `traffic` from the committed rocprofv3 PMC profile of the same config (or null)
   cpu_baseline  the compiled reference (oracle/_ref/ref_harness: ITTC/log_map.cpp's SISO and loop) on the
                 host cores, rank 0, N=1; the C restatement (oracle/) where that binary is absent
-  variants      fp32 log-MAP, fp64/fp32 Max-Log-MAP on the same batch (fewer steps)
+  variants      fp32 log-MAP, fp64/fp32 Max-Log-MAP on the same batch; BASELINE config 5 (sliding
+                window 64, overlap 30) at its own batch of 32768 (fewer steps)
 """
 from __future__ import annotations
 
@@ -32,6 +38,11 @@ sys.path.insert(0, REPO)
 
 METRIC = "decoded info Mbit/s @ K=6144, 8 iter, Eb/N0=1.0 dB; BER match vs CPU log_map"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: 6.29 TB/s measured streaming (float4 copy)
+SEED = 20261015              # srand() seed of the bench's frame stream
+CONFIG4_GLOBAL = 262144      # BASELINE config 4: 262144 codewords over 8 GPUs
+CONFIG4_PER_GPU = 32768
+CONFIG5_BATCH = 32768        # BASELINE config 5: sliding window 64, batch 32768
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (half the FP32 vector rate, 157.3 TF)
 F1, F2 = 263, 480             # QPP for K=6144 (ITTC/main.cpp:36-37)
 
@@ -41,18 +52,41 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4096, help="codewords per GPU")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="codewords per GPU (0: 4096 = config 2 at N=1, 32768 = config 4 per GPU at N>1)")
+    ap.add_argument("--strong", action="store_true",
+                    help="config 4 strong scaling: --global-batch codewords split over the N ranks")
+    ap.add_argument("--global-batch", type=int, default=CONFIG4_GLOBAL, help="total codewords with --strong")
+    ap.add_argument("--dump-bits", default="", help="directory: each rank writes its decoded slice (tests)")
     ap.add_argument("--K", type=int, default=6144)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--ebn0", type=float, default=1.0)
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--algo", default="logmap", choices=["logmap", "maxlog"])
     ap.add_argument("--cpu-sample", type=int, default=4096, help="codewords for the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the CPUs this process may use (affinity), within the box's CPU share")
     ap.add_argument("--window", type=int, default=0, help="0 = exact schedule; 64 = sliding window (config 5)")
     ap.add_argument("--overlap", type=int, default=30, help="sliding-window warm-up steps")
     ap.add_argument("--no-variants", action="store_true")
     return ap.parse_args(argv)
+
+
+def shard_layout(world: int, rank: int, batch: int, strong: bool, global_batch: int):
+    """(first global codeword, codewords) of rank `rank`.  Weak: `batch` per rank, rank r takes
+    codewords [r*batch, (r+1)*batch).  Strong: global_batch split into contiguous slices, the first
+    global_batch % world ranks one codeword more.  Codeword j is frame j of the srand(SEED) stream."""
+    if strong:
+        q, r = divmod(global_batch, world)
+        n = q + (1 if rank < r else 0)
+        return rank * q + min(rank, r), n
+    return rank * batch, batch
+
+
+def per_gpu_batch(a, world: int) -> int:
+    if a.batch:
+        return a.batch
+    return CONFIG4_PER_GPU if world > 1 else 4096
 
 
 def qpp_for(K):
@@ -84,7 +118,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from turbo_decoder_cuda_amd import TurboCodec, synth
+    from turbo_decoder_cuda_amd import TurboCodec
 
     if world > 1:
         dist.init_process_group(backend="gloo")
@@ -93,12 +127,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     f1, f2 = qpp_for(a.K)
-    u, llr_h = synth.make_batch(a.batch, a.K, f1, f2, a.ebn0, seed=20261015 + rank, dtype=np.float64)
-    llr64 = torch.from_numpy(llr_h).to(dev)
-    llr = llr64 if a.precision == "f64" else llr64.float()
-    u_d = torch.from_numpy(u).to(dev)
+    first, a.batch = shard_layout(world, rank, per_gpu_batch(a, world), a.strong, a.global_batch)
+    a.total = a.global_batch if a.strong else a.batch * world
 
     codec = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=local)
+    # this rank's slice of the global frame stream: frames [first, first + batch) of srand(SEED)
+    codec.synth_seed(SEED)
+    codec.synth_seek(first)
+    u_d, llr64 = codec.synth(a.batch, a.ebn0)
+    llr = llr64 if a.precision == "f64" else llr64.float()
     if a.window:
         codec.set_window(a.window, a.overlap)
     codec.reserve(a.batch)   # also picks the workspace placement (td_reserve)
@@ -128,6 +165,9 @@ def main():
 
     errs = int((bits != u_d).sum().item())
     blk = int((bits != u_d).any(dim=1).sum().item())
+    if a.dump_bits:
+        os.makedirs(a.dump_bits, exist_ok=True)
+        np.save(os.path.join(a.dump_bits, f"bits_rank{rank}_first{first}.npy"), bits.cpu().numpy())
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
     out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     out["workspace_placement"] = {"probe_ms": placement[0], "kept": placement[1],
@@ -136,9 +176,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_variants:
         out["pcie_inclusive"] = pcie_inclusive(a, codec, llr, dev, stream)
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(a, llr_h, bits.cpu().numpy(), f1, f2)
+        n = min(a.cpu_sample, a.batch)
+        out["cpu_baseline"] = cpu_baseline(a, llr64[:n].cpu().numpy(), bits[:n].cpu().numpy(), f1, f2)
     if rank == 0 and world == 1 and not a.no_variants:
-        out["variants"] = variants(a, llr64, u_d, f1, f2, dev, stream)
+        out["variants"] = variants(a, codec, llr64, u_d, f1, f2, dev, stream)
         out["demod"] = demod_rates(a, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -161,10 +202,40 @@ def reduce_over_ranks(elapsed: float, errs: int, blk: int, world: int):
     return float(t.item()), int(e[0]), int(e[1])
 
 
+def traffic_model(K: int, B: int, iters: int, esz: int, algo: str) -> dict:
+    """HBM bytes per turbo-kernel launch by stream, from the exact schedule's access pattern
+    (groups G = ceil(B/8), L = K+3, nT = ceil(L/12) windows, 2*iters SISOs):
+      alpha     F pass writes one 64-element row per step (log-MAP; Max-Log-MAP one in three), the
+                B pass DMAs whole 12-row windows back (log_map.cpp:975-1001 alpha, kept for the LLRs)
+      tempmax   one 8-element row per step written, whole windows read back (beta's :1019 input)
+      inputs    ys, yp, La tiles (+ write positions) staged once in the F pass, again in the B pass
+      extrinsic Le written once per SISO (8 B per element, coalesced over a group's 8 codewords)
+      sys2      the first SISO forms decoder 2's systematic input (a gather within L2, one write)
+    The sum is checked against the PMC total (FETCH_SIZE x2 + WRITE_SIZE) in profiles/traffic.json."""
+    G = (B + 7) // 8
+    L = K + 3
+    nT = (L + 11) // 12
+    S = 2 * iters
+    rows_a = L if algo == "logmap" else (L + 2) // 3
+    rows_a_read = nT * 12 if algo == "logmap" else nT * 4
+    alpha = S * G * (rows_a + rows_a_read) * 64 * esz
+    tm = S * G * (L + nT * 12) * 8 * esz
+    tile = 3 * 12 * 8 * esz + 2 * 12 * 4   # ys, yp, La rows + the window's write positions
+    inputs = S * G * 2 * nT * tile
+    ext = S * G * K * 8 * esz
+    sys2 = G * K * 8 * esz * 2
+    bits = B * K
+    parts = {"alpha": alpha, "tempmax": tm, "inputs": inputs, "extrinsic": ext, "sys2": sys2, "bits": bits}
+    total = sum(parts.values())
+    return {"bytes": parts, "total": total, "share": {k: round(v / total, 4) for k, v in parts.items()},
+            "scratch_share": round((alpha + tm) / total, 4)}
+
+
 def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2) -> dict:
     """The bench JSON record.  value = info bits decoded by ALL ranks / max-over-ranks time."""
     ms_step = elapsed / a.steps * 1e3
-    total_bits = world * a.batch * a.K * a.steps
+    total = getattr(a, "total", a.batch * world)   # codewords of all ranks per step
+    total_bits = total * a.K * a.steps
     value = total_bits / elapsed / 1e6
     esz = 8 if a.precision == "f64" else 4
     bytes_cw = esz * (3 * a.K + 12) + a.K   # algorithmic: LLR in + uint8 bits out (SURVEY.md 8d)
@@ -172,13 +243,29 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9 if turbo_ms > 0 else 0.0
     cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}" + (f"_w{a.window}g{a.overlap}" if a.window else "")
     traffic = load_traffic(cfg_key)
+    model = None if a.window else traffic_model(a.K, a.batch, a.iters, esz, a.algo)
     # measured HBM bytes (PMC) per launch over the live kernel time: what the memory system
     # actually moves (the exact kernel streams alpha / tempmax through HBM by design)
     traffic_gbs = traffic / (turbo_ms * 1e-3) / 1e9 if (traffic and turbo_ms > 0) else None
     # fp64 VALU work of the exact schedule (~133 ops per trellis step and SISO,
     # max* counted as one op) over the live kernel time
     valu_tops = a.batch * (a.K + 3) * 2 * a.iters * 133 / (turbo_ms * 1e-3) / 1e12 if turbo_ms > 0 else 0.0
-    cfg_no = "5" if a.window else ("2" if a.algo == "logmap" else "3")
+    if a.window:
+        cfg_no = "5"
+    elif world > 1 or a.batch > 4096 or a.strong:
+        cfg_no = "4"
+    else:
+        cfg_no = "2" if a.algo == "logmap" else "3"
+    if cfg_no == "4":
+        workload = (f"BASELINE config 4: {total} x K={a.K} over {world} GPU(s), "
+                    + (f"strong scaling ({a.batch} on rank 0)" if a.strong else f"{a.batch} per GPU, weak scaling")
+                    + f", {a.iters} iterations, {'log-MAP table max*' if a.algo == 'logmap' else 'Max-Log-MAP'}, "
+                    f"{a.precision}, Eb/N0={a.ebn0} dB")
+    else:
+        workload = (f"BASELINE config {cfg_no}: batch {a.batch} x K={a.K} per GPU, "
+                    f"{a.iters} iterations, {'log-MAP table max*' if a.algo == 'logmap' else 'Max-Log-MAP'}, "
+                    f"{a.precision} {'parity (reference op order)' if a.precision == 'f64' else 'throughput'}, "
+                    f"Eb/N0={a.ebn0} dB" + (f", sliding window {a.window} with overlap {a.overlap}" if a.window else ""))
     return {
         "metric": METRIC,
         "value": round(value, 3),
@@ -188,16 +275,15 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": a.precision,
-        "data": "synthetic: PCG64 info bits, RSC 13/15 + QPP turbo encoder, BPSK, AWGN (numpy), LLR=2y/sigma^2",
+        "data": (f"synthetic: ITTC/main.cpp's frames of srand({SEED}) (rand() % 2 info bits, RSC 13/15 + QPP "
+                 "turbo encoder, BPSK, mgrns AWGN, LLR = 2y/sigma^2) generated on the GPU by td_synth_frames, "
+                 "bit-identical to the reference's; global codeword j = frame j, each rank decodes its slice"),
         "config": {
-            "workload": f"BASELINE config {cfg_no}: batch {a.batch} x K={a.K} per GPU, "
-                        f"{a.iters} iterations, {'log-MAP table max*' if a.algo == 'logmap' else 'Max-Log-MAP'}, "
-                        f"{a.precision} {'parity (reference op order)' if a.precision == 'f64' else 'throughput'}, "
-                        f"Eb/N0={a.ebn0} dB" + (f", sliding window {a.window} with overlap {a.overlap}" if a.window else ""),
-            "K": a.K, "f1": f1, "f2": f2, "batch_per_gpu": a.batch, "global_batch": a.batch * world,
+            "workload": workload,
+            "K": a.K, "f1": f1, "f2": f2, "batch_per_gpu": a.batch, "global_batch": total,
             "iterations": a.iters, "algo": a.algo, "precision": a.precision, "ebn0_db": a.ebn0,
             "window": a.window, "overlap": a.overlap if a.window else None,
             "parallelism": f"batch-shard x{world} (no collective on the data path)",
@@ -212,6 +298,9 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
             "traffic": traffic,
             "traffic_gbs": round(traffic_gbs, 1) if traffic_gbs else None,
             "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
+            "traffic_frac_measured_ceiling": round(traffic_gbs / HBM_MEASURED_GBS, 4) if traffic_gbs else None,
+            "measured_ceiling_gbs": HBM_MEASURED_GBS,
+            "traffic_model": model,
             "limiter": ("latency of the serial alpha / beta recursions (one dependent trellis step at a time "
                         "per codeword; DESIGN.md 3.2): neither HBM nor VALU is saturated") if not a.window else
                        "VALU / LDS issue of the sub-block chains (DESIGN.md 8.3)",
@@ -230,54 +319,73 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
 REF_HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
 
 
+def cpu_threads(a) -> dict:
+    """Threads for the CPU baseline: every CPU this process may run on (sched_getaffinity), within
+    the box's CPU share when the harness sets one (OMP_NUM_THREADS: 16 for a one-GPU lease, whose
+    affinity can still list the whole machine).  Physical cores are reported beside it."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(share) if share.isdigit() and int(share) > 0 else 0
+    threads = a.cpu_threads or (min(avail, share) if share else avail)
+    return {"threads": threads, "affinity_cpus": avail, "cpu_share": share or None,
+            "physical_cores": _physical_cores()}
+
+
 def cpu_baseline(a, llr_h, gpu_bits, f1, f2):
     """The reference's CPU path on the host cores, over the first `cpu_sample` codewords of the
     same batch.  fp64 log-MAP: the compiled reference itself (oracle/_ref/ref_harness, built from
     /root/reference/ITTC/log_map.cpp by `make -C oracle ref`; its `decode` mode runs TurboDecoding's
     loop through the reference's functions, frames spread over threads) -- kind "reference".
     Otherwise, or where that binary was not built: the C restatement (oracle/) -- kind "port"."""
-    n = min(a.cpu_sample, a.batch)
-    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    n = llr_h.shape[0]
+    ct = cpu_threads(a)
+    threads = ct["threads"]
     if a.precision == "f64" and a.algo == "logmap" and os.access(REF_HARNESS, os.X_OK):
         import subprocess
         import tempfile
 
         with tempfile.TemporaryDirectory() as td:
             fin, fout = os.path.join(td, "flows.bin"), os.path.join(td, "bits.bin")
-            np.ascontiguousarray(llr_h[:n], dtype=np.float64).tofile(fin)
+            np.ascontiguousarray(llr_h, dtype=np.float64).tofile(fin)
             r = subprocess.run([REF_HARNESS, "decode", str(a.K), str(f1), str(f2), str(a.iters), str(threads), fin, fout],
                                capture_output=True, text=True, check=True)
             dt = float(r.stdout.split()[1])
             cb = np.fromfile(fout, dtype=np.uint8).reshape(n, a.K)
-        return {
-            "value": round(n * a.K / dt / 1e6, 4),
-            "unit": "Mbit/s",
-            "cores": threads,
-            "kind": "reference",
-            "sample": f"{n} codewords of the same batch (K={a.K}, {a.iters} iter, fp64 log-MAP) through the compiled "
-                      f"reference (ITTC/log_map.cpp, g++ -O2), {threads} threads, {dt:.2f} s",
-            "bits_match_gpu": bool(np.array_equal(cb, gpu_bits[:n])),
-            "cpu_model": _cpu_model(),
-        }
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pyoracle
+        kind, what = "reference", "the compiled reference (ITTC/log_map.cpp, g++ -O2)"
+    else:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import pyoracle
 
-    sample = np.ascontiguousarray(llr_h[:n])
-    if a.precision == "f32":
-        sample = sample.astype(np.float32)
-    algo = pyoracle.ALGO_LOGMAP if a.algo == "logmap" else pyoracle.ALGO_MAXLOG
-    t0 = time.perf_counter()
-    cb = pyoracle.decode_batch(sample, a.K, f1, f2, a.iters, algo, nthreads=threads)
-    dt = time.perf_counter() - t0
+        sample = np.ascontiguousarray(llr_h)
+        if a.precision == "f32":
+            sample = sample.astype(np.float32)
+        algo = pyoracle.ALGO_LOGMAP if a.algo == "logmap" else pyoracle.ALGO_MAXLOG
+        t0 = time.perf_counter()
+        cb = pyoracle.decode_batch(sample, a.K, f1, f2, a.iters, algo, nthreads=threads)
+        dt = time.perf_counter() - t0
+        kind, what = "port", "the C restatement (oracle/turbo_oracle.c)"
+    value = n * a.K / dt / 1e6
+    per_core = value / threads
     return {
-        "value": round(n * a.K / dt / 1e6, 4),
+        "value": round(value, 4),
         "unit": "Mbit/s",
         "cores": threads,
-        "kind": "port",
-        "sample": f"{n} codewords of the same batch (K={a.K}, {a.iters} iter, {a.precision} {a.algo}), "
-                  f"{threads} threads, {dt:.2f} s",
-        "bits_match_gpu": bool(np.array_equal(cb, gpu_bits[:n])),
+        "kind": kind,
+        "sample": f"{n} codewords of the same batch (K={a.K}, {a.iters} iter, {a.precision} {a.algo}) through {what}, "
+                  f"one frame per thread, {threads} threads, {dt:.2f} s",
+        "bits_match_gpu": bool(np.array_equal(cb, gpu_bits)),
         "cpu_model": _cpu_model(),
+        "affinity_cpus": ct["affinity_cpus"],
+        "cpu_share": ct["cpu_share"],
+        "physical_cores": ct["physical_cores"],
+        "per_core": round(per_core, 4),
+        "all_physical_cores_extrapolated": (round(per_core * ct["physical_cores"], 3) if ct["physical_cores"] else None),
+        "note": "threads = the CPUs this process may use within the box's CPU share (OMP_NUM_THREADS on a one-GPU "
+                "lease); frames are independent, so the rate scales with threads (all_physical_cores_extrapolated "
+                "= per_core x physical cores, an extrapolation, not a measurement)",
     }
 
 
@@ -339,7 +447,10 @@ def pcie_inclusive(a, codec, llr, dev, stream):
                     "pipeline (H2D and D2H on copy streams under the decode); serial: one stream"}
 
 
-def variants(a, llr64, u_d, f1, f2, dev, stream):
+def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
+    """Other arithmetic modes on the same batch (configs 3, fp32), and BASELINE config 5 (sliding
+    window 64 with overlap 30) at its own batch of 32768 codewords: frames 0..32767 of the same
+    srand(SEED) stream, made on the device by the bench's codec."""
     import torch
 
     from turbo_decoder_cuda_amd import TurboCodec
@@ -347,15 +458,25 @@ def variants(a, llr64, u_d, f1, f2, dev, stream):
     res = {}
     cases = [(p, g, 0) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog"))]
     cases += [(p, g, 64) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
+    big = None
     for prec, algo, win in cases:
         if prec == a.precision and algo == a.algo and win == a.window:
             continue
-        x = llr64 if prec == "f64" else llr64.float()
+        if win:
+            if big is None:   # config 5's batch, once for the three windowed modes
+                B5 = CONFIG5_BATCH
+                codec.synth_seek(0)
+                big = codec.synth(B5, a.ebn0)
+            ub, xb = big
+            B = ub.shape[0]
+        else:
+            ub, xb, B = u_d, llr64, a.batch
+        x = xb if prec == "f64" else xb.float()
         c = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=algo, precision=prec, device=dev.index)
         if win:
             c.set_window(win, a.overlap)
-        c.reserve(a.batch)
-        b = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
+        c.reserve(B)
+        b = torch.empty((B, a.K), dtype=torch.uint8, device=dev)
         c.decode(x, b, stream=stream)
         torch.cuda.synchronize(dev)
         steps = max(2, a.steps // 2)
@@ -367,10 +488,12 @@ def variants(a, llr64, u_d, f1, f2, dev, stream):
         dt = time.perf_counter() - t0
         _, kms, _ = c.kernel_ms()
         c.close()
-        errs = int((b != u_d).sum().item())
-        res[f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else "")] = {"value": round(a.batch * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s",
-                                 "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4),
-                                 "bit_errors": errs}
+        errs = int((b != ub).sum().item())
+        del x
+        key = f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else "")
+        res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B,
+                    "config": "5" if win else ("3" if algo == "maxlog" and prec == "f64" else None),
+                    "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
     return res
 
 
@@ -400,6 +523,27 @@ def demod_rates(a, dev):
                         "GB_per_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
         del yi, yq, out
     return res
+
+
+def _physical_cores():
+    """Physical cores of the host (distinct (physical id, core id) pairs of /proc/cpuinfo)."""
+    try:
+        cores, phys, core = set(), None, None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip():
+                    if core is not None:
+                        cores.add((phys, core))
+                    phys = core = None
+        if core is not None:
+            cores.add((phys, core))
+        return len(cores) or None
+    except OSError:
+        return None
 
 
 def _cpu_model():

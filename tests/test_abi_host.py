@@ -229,3 +229,16 @@ def test_decode_output_buffer_checks():
     for t in bad:
         with pytest.raises(ValueError):
             chk("bits", t, torch.uint8, (4, 8), dev)
+
+
+def test_multi_gpu_example_builds(tmp_path):
+    """examples/multi_gpu_decode.cpp (one handle + thread + stream per device ordinal) compiles and
+    links against the C ABI with plain g++ and the HIP runtime headers (run: tests/test_gpu_multidevice.py)."""
+    pkg = os.path.join(REPO, "turbo_decoder_cuda_amd")
+    out = str(tmp_path / "mgd")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", f"-I{REPO}/include",
+                           "-I/opt/rocm/include", os.path.join(REPO, "examples", "multi_gpu_decode.cpp"),
+                           f"-L{pkg}", "-lturbo_mi355x", "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
+                           f"-Wl,-rpath,{pkg}", "-Wl,-rpath,/opt/rocm/lib", "-o", out])
+    r = subprocess.run([out], capture_output=True, text=True)
+    assert r.returncode == 2 and "usage" in r.stderr

@@ -52,3 +52,42 @@ def test_gloo_two_ranks():
         assert rec["config"]["global_batch"] == 128
         assert rec["ber"]["bit_errors"] == 13
         assert rec["roofline"]["alg_bytes_per_codeword"] == 8 * (3 * 1024 + 12) + 1024
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_layout_partitions_the_global_batch(world):
+    """bench.shard_layout: the ranks' slices of the global frame stream are contiguous, disjoint
+    and cover it exactly -- weak (a fixed batch per rank; N=8 x 32768 = config 4's 262144) and
+    strong (one global batch split, remainder to the first ranks)."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+
+    for strong, batch, total in ((False, 32768, 32768 * world), (False, 45, 45 * world), (True, 0, 262144),
+                                 (True, 0, 91), (True, 0, 7)):
+        sl = [bench.shard_layout(world, r, batch, strong, total) for r in range(world)]
+        pos = 0
+        for first, n in sl:
+            assert first == pos and n >= 0
+            pos += n
+        assert pos == total
+        if strong:
+            ns = [n for _, n in sl]
+            assert max(ns) - min(ns) <= 1
+    a = bench.parse([])
+    assert bench.per_gpu_batch(a, 1) == 4096 and bench.per_gpu_batch(a, 8) == 32768
+    assert 8 * bench.per_gpu_batch(a, 8) == bench.CONFIG4_GLOBAL
+
+
+def test_traffic_model_matches_the_pmc_total():
+    """The per-stream HBM model of the exact kernel (bench.traffic_model) against the PMC bytes
+    per launch committed in profiles/traffic.json (config 2): within 2 %, alpha the largest share."""
+    import json
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+
+    m = bench.traffic_model(6144, 4096, 8, 8, "logmap")
+    pmc = json.load(open(os.path.join(REPO, "profiles", "traffic.json")))["K6144_B4096_it8_f64_logmap"]
+    assert abs(m["total"] / pmc["bytes_per_launch"] - 1) < 0.02
+    assert max(m["bytes"], key=m["bytes"].get) == "alpha"

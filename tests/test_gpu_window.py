@@ -133,3 +133,47 @@ def test_reference_gpu_decoder_ber_matches_published():
             print(pub[k]["ebn0_db"], ber, pub[k]["ber"][9], fer, pub[k]["fer"][9])
             assert abs(ber / pub[k]["ber"][9] - 1) < 0.25
             assert abs(fer / pub[k]["fer"][9] - 1) < 0.25
+
+
+@pytest.mark.timeout(300)
+def test_config5_full_batch():
+    """BASELINE config 5 at its stated size: K=6144, sliding window 64 with overlap 30, batch
+    32768 of main.cpp's frames (device generator) at 1.0 dB, 8 iterations.
+      * fp64 log-MAP (the bench's config-5 line): residual bit errors within the exact schedule's
+        on the same frames plus a margin (the windowed arithmetic differs by construction);
+      * fp64 Max-Log-MAP on the same batch: two seeded codewords equal to oracle/window_oracle.py
+        (the restatement of the reference's sub-block decoder, turboDecoderBianJieZhi.cu:248,
+        302-304, 397-400) -- every iteration's bits, Le within 1e-9."""
+    import torch
+
+    import window_oracle as WO
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2, B, iters = 6144, 263, 480, 32768, 8
+    errs = {}
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.synth_seed(20261015)
+        info, llr = c.synth(B, 1.0)
+        for mode in ("exact", "window"):
+            c.set_window(64 if mode == "window" else 0, 30, 1.0)
+            c.reserve(B)
+            bits = c.decode(llr)
+            torch.cuda.synchronize()
+            errs[mode] = int((bits != info).sum().item())
+            del bits
+    print(errs)
+    assert errs["window"] <= 1.5 * errs["exact"] + 100
+    sample = np.random.default_rng(5).choice(B, 2, replace=False)
+    with TurboCodec(K, f1, f2, iterations=iters, algo="maxlog") as c:
+        c.set_window(64, 30, 1.0)
+        c.reserve(B)
+        bits = torch.empty((B, iters, K), dtype=torch.uint8, device=llr.device)
+        le = torch.empty((B, iters, 2, K + 3), dtype=torch.float64, device=llr.device)
+        c.decode(llr, bits, all_iters=True, le=le)
+        torch.cuda.synchronize()
+        idx = torch.from_numpy(sample).to(llr.device)
+        bs, ls, fs = bits[idx].cpu().numpy(), le[idx].cpu().numpy(), llr[idx].cpu().numpy()
+    del bits, le, llr, info
+    for k in range(len(sample)):
+        ob, ol = WO.turbo_decode_window(fs[k], K, f1, f2, iters, 64, 30)
+        assert np.array_equal(bs[k], ob), f"codeword {sample[k]}"
+        assert np.abs(ls[k] - ol).max() <= 1e-9, f"codeword {sample[k]}"
