@@ -65,9 +65,13 @@ int td_destroy(td_handle* h);
  * into a hipGraph. */
 int td_reserve(td_handle* h, int B);
 /* td_reserve of the exact schedule for B >= 1024 also picks the workspace's placement: the turbo
- * kernel's speed depends on the physical pages behind it (two modes 6-7 % apart on MI355X), so it
- * times one iteration on candidate workspaces (up to TD_PLACEMENT_TRIALS, environment variable,
- * default 24; 1 = a plain allocation; stopping once both modes were seen) and keeps the fastest.
+ * kernel's speed depends on the physical pages behind it (two modes 6-7 % apart on MI355X; the
+ * slow one shows 5-8x the DRAM credit stalls), so it times one iteration on candidate workspaces
+ * and keeps the fastest.  Up to TD_PLACEMENT_TRIALS candidates (environment variable, default 24;
+ * 1 = a plain allocation); the search stops once one candidate runs >= 4 % below the median of
+ * those timed (at least three), never on a slow straggler.  Transient memory: every candidate is
+ * held until the choice (so each gets fresh pages), at most half the free device memory and at
+ * most 96 GiB in total (config 2: ~2.4 GiB a candidate; a 32768-codeword batch: ~19 GiB).
  * Results do not depend on it. */
 
 /*
@@ -83,7 +87,11 @@ int td_reserve(td_handle* h, int B);
  * A handle owns ONE device workspace: decodes on one handle never overlap.  A decode issued on a
  * different stream than the previous one waits on the device (hipStreamWaitEvent) until the
  * previous decode is done with the workspace; for concurrent decodes use one handle per stream.
- * A handle is not thread-safe: one host thread uses it at a time.
+ * A decode captured into a hipGraph (stream capture) neither waits on nor records that event, so
+ * graph replays are not ordered against eager decodes on the same handle: issue them on one
+ * stream, or order them with events.  Call td_reserve before capturing (no allocation inside).
+ * A handle is not thread-safe: one host thread uses it at a time; handles on different threads
+ * (and devices) are independent (examples/multi_gpu_decode.cpp).
  */
 int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                      void* stream);
@@ -187,7 +195,7 @@ int td_abi_version(void);
 
 /*
  * Host evaluation of the exact bucket form of E_algorithm used on the device (no GPU needed):
- * max(x,y) + table(|y-x|) through the 57-bucket LUT the kernels read from LDS.  Lets CPU
+ * max(x,y) + table(|y-x|) through the 29-bucket LUT the kernels read from LDS.  Lets CPU
  * tests prove LUT == log_map.cpp:779-801 for every threshold.  algo = enum td_algo.
  */
 double td_maxstar_host_f64(double x, double y, int algo);

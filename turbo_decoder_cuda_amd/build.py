@@ -64,8 +64,8 @@ def build(force: bool = False, verbose: bool = False) -> None:
         _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-shared", "-o", LIB, *srcs], verbose)
     stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
     if force or _newer(stamps, deps):
-        # the stamp build keeps the generic beta loop: with the stamps the dedicated one spills
-        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-DTD_BETA_FAST=0", "-shared", "-o", stamps, *srcs], False)
+        # the same schedule as the production build (the dedicated beta loop fits since round 3)
+        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-shared", "-o", stamps, *srcs], False)
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,

@@ -331,11 +331,13 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
     return best;
 }
 
-// Stop rule of the placement search: the fast mode has been seen once some candidate runs >= 4 %
+// Stop rule of the placement search: the fast mode has been seen once (a) some candidate runs >= 4 %
 // below the median of all candidates probed so far (at least three, so that the median is a mode and
-// not an average of the two).  A slow straggler never stops the search: with every candidate in
-// the slow mode the median is slow too and nothing is 4 % below it.  (Until round 3 the rule was
-// "two candidates differ by 4 %", which an upward outlier among slow candidates satisfied.)
+// not an average of the two), or (b) at least three candidates run >= 4 % slower than the best one
+// (the slow mode confirmed three times, so the best is not merely the fast side of one straggler).
+// A slow straggler never stops the search: with every candidate in the slow mode the median is
+// slow too and nothing is 4 % below it.  (Until round 3 the rule was "two candidates differ by
+// 4 %", which an upward outlier among slow candidates satisfied.)
 bool placement_fast_seen(const std::vector<float>& ms)
 {
     std::vector<float> v;
@@ -344,12 +346,17 @@ bool placement_fast_seen(const std::vector<float>& ms)
     if (v.size() < 3) return false;
     std::sort(v.begin(), v.end());
     const float med = v.size() % 2 ? v[v.size() / 2] : 0.5f * (v[v.size() / 2 - 1] + v[v.size() / 2]);
-    return v.front() < 0.96f * med;
+    if (v.front() < 0.96f * med) return true;
+    int slower = 0;
+    for (float x : v) slower += x >= 1.04f * v.front();
+    return slower >= 3;
 }
 
 // Candidate workspaces the search may hold at once: half the free device memory, and at most
-// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.
-constexpr size_t kPlaceHoldBytes = (size_t)48 << 30;
+// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  96 GiB
+// lets config 4's 32768-codeword shard (19 GiB a workspace) try five candidates: with two (the
+// 48 GiB cap of round 3's first runs) both landed in the slow mode (18.96 / 18.58 ms probes).
+constexpr size_t kPlaceHoldBytes = (size_t)96 << 30;
 
 int place_ws(td_handle* h, int G)
 {

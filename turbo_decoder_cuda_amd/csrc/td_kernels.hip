@@ -14,15 +14,18 @@
 // alpha/beta critical path except the max* table (one ds_read per max*).
 //
 // SISO = Log_MAP_decoder (ITTC/log_map.cpp:898-1047) in the serial schedule of TurboDecoding
-// (:1217-1265).  Per SISO:
-//   F pass  alpha forward over the L = K+3 steps, alpha checkpoint every W steps (HBM scratch);
-//   B pass  windows last..first.  beta of window t runs fused with the alpha recompute of
-//           window t-1 (two independent chains per step); the recompute stores per step and
-//           state the sums (gamma + alpha) entering the max* (= the LLR terms, :1028-1034) and
-//           the reference's tempmax, beta subtracts tempmax[i+1] (:1019) and adds itself into
-//           the stored sums; then the LLR folds E_seq(temp1) - E_seq(temp0) run over
-//           (step, codeword) items in state order 0..7 (:1038) and the extrinsic update
-//           Le = LLR - La - 2*ys (:1237, :1258) is written out.
+// (:1217-1265).  Per SISO, over windows of kW = 12 trellis steps:
+//   F pass  wave A runs alpha forward over the L = K+3 steps and streams alpha of EVERY step (by
+//           state, 512 B per group and step in fp64) and the reference's tempmax (:986-993) to an
+//           HBM scratch (astore / tmstore); Max-Log-MAP stores alpha one step in three and the
+//           folds recompute the steps in between.  No alpha is recomputed in log-MAP.
+//   B pass  windows last..first in a three-stage pipeline: wave B runs beta of window t
+//           (subtracting tempmax[i+1], :1019, staged in LDS) and publishes beta by state; the
+//           loader DMAs the alpha rows of window t-1 from the scratch into an LDS ring; the two
+//           fold waves run the LLR folds E_seq(temp1) - E_seq(temp0) of window t+1 over
+//           (step, codeword) items in state order 0..7 (:1038) and write the extrinsic update
+//           Le = LLR - La - 2*ys (:1237, :1258) at the interleaved position.
+// The scratch stream is ~70 % of the kernel's HBM traffic (bench.py traffic_model).
 // Every floating-point operation is the reference's, in the reference's order (max* is
 // symmetric, so the two operands may arrive in either order).  Build with -ffp-contract=off.
 #include <hip/hip_runtime.h>
