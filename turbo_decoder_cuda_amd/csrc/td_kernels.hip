@@ -454,6 +454,12 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
 }
 
 // dma16 with a wave-uniform SGPR base and a per-lane 32-bit byte offset (saddr form)
+// alpha_dma through dma16_s: 17 VGPRs fewer in the fp64 log-MAP kernel (256 -> 239), but 0.9 %
+// slower on one box (17.47 vs 17.31 ms, 3 interleaved rounds), so the per-lane 64-bit form stays the
+// default; the step-major alpha layout (TD_AWIN 2) needs the saddr form.
+#ifndef TD_ADMA_SADDR
+#define TD_ADMA_SADDR (TD_AWIN == 2)
+#endif
 __device__ __forceinline__ void dma16_s(unsigned lds, const void* sbase, unsigned voff)
 {
     unsigned save;
@@ -604,12 +610,12 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
-    // The window's rows are arow_bytes apart (step-major: G groups; else contiguous).  Each DMA
-    // covers rpd LDS rows; its first source row is a wave-uniform SGPR base, the lane's row and
-    // chunk within it a 32-bit offset (saddr form: no 64-bit per-lane addresses, 17 VGPRs fewer
-    // in the fp64 log-MAP kernel than per-lane pointers).  LDS row r holds the window's step r
-    // (max-log: ck_step(r)); chunk pc of codeword block cb holds the block's chunk
+    // saddr form (TD_ADMA_SADDR): the window's rows are arow_bytes apart (step-major: G groups;
+    // else contiguous).  Each DMA covers rpd LDS rows; its first source row is a wave-uniform SGPR
+    // base, the lane's row and chunk within it a 32-bit offset.  LDS row r holds the window's step
+    // r (max-log: ck_step(r)); chunk pc of codeword block cb holds the block's chunk
     // (pc - av_rot) mod kBlkChunks (blk_off).
+#if TD_ADMA_SADDR
     const unsigned arow_bytes = (unsigned)(astore_row_stride(gm.G) * sizeof(T));
     constexpr int lpr = row_bytes / 16, rpd = kLanes / lpr;   // lanes per row, rows per DMA
 #pragma unroll
@@ -625,6 +631,21 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
         const int sr = ALGO == 1 ? ck_step(r) : r;
         dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
     }
+#else   // round-2 form: a 64-bit per-lane source pointer per DMA (contiguous rows only)
+    static_assert(TD_AWIN != 2, "the per-lane form assumes contiguous window rows");
+#pragma unroll
+    for (int q = 0; q < n; ++q) {
+        const int b = q * kDmaBytes + lane * 16;
+        int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
+        if constexpr (kFoldSwz<T>) {
+            const int r = b / row_bytes, w = b % row_bytes;
+            constexpr int blk = 8 * (int)sizeof(T);
+            const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
+            off = (ALGO == 1 ? ck_step(r) : r) * row_bytes + (w / blk) * blk + pc * 16;
+        }
+        dma16(lds + q * kDmaBytes, src + off);
+    }
+#endif
 }
 
 // ---- recursion steps
