@@ -494,7 +494,46 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B,
                     "config": "5" if win else ("3" if algo == "maxlog" and prec == "f64" else None),
                     "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
+    if big is not None and a.K == 6144:
+        res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
     return res
+
+
+def ref_gpu_schedule(a, big, f1, f2, dev, stream, P=32, iters=10):
+    """Context only (not the metric): the reference's own CUDA decoder's schedule
+    (ITTC/CUDA/turboDecoderBianJieZhi.cu: Max-Log-MAP fp32, P sub-blocks of 6144/P with NII
+    boundaries, both SISOs concurrent, Le x 0.77) at 10 iterations -- the conditions of its
+    published throughput, 73.18 Mbit/s at Eb/N0 = 1.0 dB for P = 32 on a GeForce GTX 550 Ti,
+    one frame at a time, counting K+3 bits (FinalResult/throughoutput/8_4Blocks_Bian_Max_10000Fs06_20.txt:376).
+    Here: td_set_window(6144/P, 0, 0.77, nii, concurrent) on a batch of 32768 of the bench's frames."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+
+    ub, xb = big
+    B = ub.shape[0]
+    x = xb.float()
+    c = TurboCodec(a.K, f1, f2, iterations=iters, algo="maxlog", precision="f32", device=dev.index)
+    c.set_window(a.K // P, 0, 0.77, nii=True, concurrent=True)
+    c.reserve(B)
+    b = torch.empty((B, a.K), dtype=torch.uint8, device=dev)
+    c.decode(x, b, stream=stream)
+    torch.cuda.synchronize(dev)
+    steps = max(2, a.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        c.decode(x, b, stream=stream)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    c.close()
+    errs = int((b != ub).sum().item())
+    del x
+    return {"value": round(B * a.K / dt / 1e6, 3), "unit": "Mbit/s", "value_k_plus_3": round(B * (a.K + 3) / dt / 1e6, 3),
+            "batch": B, "iterations": iters, "P": P, "ms_per_step": round(dt * 1e3, 4), "bit_errors": errs,
+            "reference_published": {"value": 73.18, "unit": "Mbit/s (K+3 bits)", "hardware": "GeForce GTX 550 Ti, one frame",
+                                    "source": "ITTC/CUDA/FinalResult/throughoutput/8_4Blocks_Bian_Max_10000Fs06_20.txt:376"},
+            "note": "context only: a different decoder (max-log fp32, sub-blocks, 0.77 scaling; ~0.5 dB worse BER) "
+                    "from the metric's exact log-MAP path"}
 
 
 def demod_rates(a, dev):

@@ -247,6 +247,9 @@ static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 #endif
 template <int ALGO>
 constexpr int kFoldA = ALGO == 0 ? TD_FOLD_A : kFoldPerWave;
+#ifndef TD_ML_FOLD_MAP
+#define TD_ML_FOLD_MAP 1   // Max-Log-MAP fold items split by recompute depth (siso_wg B pass)
+#endif
 static_assert(TD_FOLD_A <= kLanes && kTile - TD_FOLD_A <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 
@@ -1659,8 +1662,17 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     } else {
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
-        const int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
-        const int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
+        int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
+        int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
+        if constexpr (ALGO == 1 && TD_ML_FOLD_MAP && kCkPhases == 1) {
+            // Max-Log-MAP items by recompute depth (alpha stored at k = 0 mod 3): the fold wave
+            // beside the other workgroup's beta (F1) takes the steps k = 0, 1 mod 3 (64 items, at
+            // most one recomputed step), wave A (beside the loader) the steps k = 2 mod 3 (32 items,
+            // two).  With items in step order every wave paid two recomputed steps.
+            const int q = lane >> 3;
+            fe = wave == 0 ? (3 * q + 2) * kCw + (lane & 7) : (3 * (q >> 1) + (q & 1)) * kCw + (lane & 7);
+            nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
+        }
         int j0 = 0;
         if (TD_FOLD_FAST && ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
