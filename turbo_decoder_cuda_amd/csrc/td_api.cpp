@@ -919,6 +919,18 @@ int td_debug_placement(td_handle* h, float* ms, int cap, int* pick)
 }
 
 #ifdef TD_WS_EXPERIMENT
+// Diagnostics build only (not in the header): the workspace allocation and the byte offset of the
+// alpha scratch inside it (scripts/ws_copy_probe.py streams through it to time plain copies).
+int td_debug_ws(td_handle* h, void** ptr, size_t* bytes, size_t* astore_off)
+{
+    if (!h || !h->d_ws) return fail(TD_EINVAL, "td_debug_ws: no workspace");
+    const Carve c = carve(h->ws_groups, h->p.K, h->elem);
+    *ptr = h->d_ws;
+    *bytes = h->ws_bytes;
+    *astore_off = c.astore;
+    return TD_OK;
+}
+
 // Diagnostics build only (not in the header): swap workspace arrays between two handles of the same
 // K, precision and reserved batch, to find which array carries the placement mode.
 // mask bits 0-7: sys1 par1 sys2 par2 ext12 ext21 astore tmstore; bit 8: pi + pinv; bit 9: the
