@@ -44,6 +44,31 @@ constexpr int kLanes = 64;
 constexpr int kTile = kW * kCw;                 // (step, codeword) elements per window
 static_assert(kW % 3 == 0, "window must be a multiple of the label period");
 
+// Alpha rows kept in the F pass -> B pass scratch, by phase i mod 3 (bit p: steps i = p mod 3).
+#ifndef TD_CK_PHASES
+#define TD_CK_PHASES 1   // bit p: alpha of the steps i = p mod 3 is stored (max-log)
+#endif
+// Log-MAP may store a subset of the rows as well (TD_CK_PHASES_LOGMAP; 7 = every row, the
+// default): the folds then recompute the missing rows with the table max*, bit-identical to the
+// alpha wave (alpha_recompute), in exchange for less scratch traffic.
+#ifndef TD_CK_PHASES_LOGMAP
+#define TD_CK_PHASES_LOGMAP 7
+#endif
+constexpr int kCkPhases = TD_CK_PHASES | 1;
+template <int ALGO>
+constexpr int kCkPh = ALGO == 1 ? kCkPhases : (TD_CK_PHASES_LOGMAP | 1);   // stored phases of this algorithm
+template <int ALGO>
+constexpr bool kCkAll = kCkPh<ALGO> == 7;                                    // every row stored
+// the phase whose steps sit furthest from a kept row (recomputed through the most steps)
+constexpr int ck_depth(int ph, int p)
+{
+    int d = 0;
+    while (!((ph >> p) & 1)) --p, ++d;
+    return d;
+}
+template <int ALGO>
+constexpr int kCkDeepest = ck_depth(kCkPh<ALGO>, 2) >= ck_depth(kCkPh<ALGO>, 1) ? 2 : 1;
+
 // ------------------------------------------------------------------ DPP helpers
 constexpr int kDppXor1 = 0xB1;    // quad_perm [1,0,3,2]
 constexpr int kDppXor2 = 0x4E;    // quad_perm [2,3,0,1]
@@ -329,7 +354,7 @@ __device__ __forceinline__ void load_block(const T* blk, int r, T (&v)[8])
 template <int ALGO>
 __device__ __forceinline__ int av_rot(int r, int c)
 {
-    return (ALGO == 1 && TD_MLAV_ROT) ? r + 2 * (c >> 2) : r;
+    return (!kCkAll<ALGO> && TD_MLAV_ROT) ? r + 2 * (c >> 2) : r;
 }
 // row offset 8c + s (st_off) -> rotated
 template <typename T>
@@ -571,36 +596,37 @@ static_assert(kMemory + kW - 2 < kPermPad, "write-position chunks stay within th
 // and the folds recompute the steps in between from the last stored one (alpha_recompute): less
 // alpha traffic, which otherwise bounds its forward pass (HBM writes).  The copy gathers the
 // window's stored rows into consecutive LDS rows.
-#ifndef TD_CK_PHASES
-#define TD_CK_PHASES 1   // bit p: alpha of the steps i = p mod 3 is stored (max-log)
-#endif
-constexpr int kCkPhases = TD_CK_PHASES | 1;
-constexpr int kCkPerGroup = (kCkPhases & 1) + ((kCkPhases >> 1) & 1) + ((kCkPhases >> 2) & 1);
-constexpr int kCkRows = kW / 3 * kCkPerGroup;   // stored rows per window
+// (TD_CK_PHASES / TD_CK_PHASES_LOGMAP, kCkPh, kCkAll: see the top of the file)
+template <int ALGO>
+constexpr int kCkPerGroup = (kCkPh<ALGO> & 1) + ((kCkPh<ALGO> >> 1) & 1) + ((kCkPh<ALGO> >> 2) & 1);
+template <int ALGO>
+constexpr int kCkRows = kW / 3 * kCkPerGroup<ALGO>;   // stored rows per window
 // window-relative step of stored row r, and the stored row at or before step k (with its step)
+template <int ALGO>
 __host__ __device__ constexpr int ck_step(int r)
 {
-    int m = r % kCkPerGroup, p = 0;
+    int m = r % kCkPerGroup<ALGO>, p = 0;
     for (; p < 3; ++p)
-        if ((kCkPhases >> p) & 1) {
+        if ((kCkPh<ALGO> >> p) & 1) {
             if (m == 0) break;
             --m;
         }
-    return 3 * (r / kCkPerGroup) + p;
+    return 3 * (r / kCkPerGroup<ALGO>) + p;
 }
+template <int ALGO>
 __device__ __forceinline__ int ck_row_of(int k, int& ks)
 {
     int p = k % 3;
-    while (!((kCkPhases >> p) & 1)) --p;   // phase 0 is always stored
+    while (!((kCkPh<ALGO> >> p) & 1)) --p;   // phase 0 is always stored
     ks = k - (k % 3) + p;
     int m = 0;
-    for (int q = 0; q < p; ++q) m += (kCkPhases >> q) & 1;
-    return (k / 3) * kCkPerGroup + m;
+    for (int q = 0; q < p; ++q) m += (kCkPh<ALGO> >> q) & 1;
+    return (k / 3) * kCkPerGroup<ALGO> + m;
 }
 template <typename T, int ALGO>
 constexpr int alpha_dma_count()
 {
-    return (ALGO == 1 ? kCkRows : kW) * kLanes * (int)sizeof(T) / (kLanes * 16);
+    return kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
 }
 static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
@@ -630,8 +656,8 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
             wo = (w / blk) * blk + pc * 16;
         }
-        const int s0 = ALGO == 1 ? ck_step(q * rpd) : q * rpd;   // source step of the DMA's first row
-        const int sr = ALGO == 1 ? ck_step(r) : r;
+        const int s0 = ck_step<ALGO>(q * rpd);   // source step of the DMA's first row
+        const int sr = ck_step<ALGO>(r);
         dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
     }
 #else   // round-2 form: a 64-bit per-lane source pointer per DMA (contiguous rows only)
@@ -639,12 +665,12 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
 #pragma unroll
     for (int q = 0; q < n; ++q) {
         const int b = q * kDmaBytes + lane * 16;
-        int off = ALGO == 1 ? ck_step(b / row_bytes) * row_bytes + b % row_bytes : b;
+        int off = ck_step<ALGO>(b / row_bytes) * row_bytes + b % row_bytes;
         if constexpr (kFoldSwz<T>) {
             const int r = b / row_bytes, w = b % row_bytes;
             constexpr int blk = 8 * (int)sizeof(T);
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
-            off = (ALGO == 1 ? ck_step(r) : r) * row_bytes + (w / blk) * blk + pc * 16;
+            off = ck_step<ALGO>(r) * row_bytes + (w / blk) * blk + pc * 16;
         }
         dma16(lds + q * kDmaBytes, src + off);
     }
@@ -709,7 +735,7 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
 #ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
     if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
 #else
-    if (ALGO == 0 || ((kCkPhases >> PH) & 1)) gstore(pa, alpha);   // in the table read's shadow; max-log: kCkPhases
+    if ((kCkPh<ALGO> >> PH) & 1) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
 #endif
     gstore(ptm, m);
     return h;
@@ -843,7 +869,7 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        gstore(ga + K * arow + lc.st_off[PH], alpha);
+        if constexpr ((kCkPh<0> >> PH) & 1) gstore(ga + K * arow + lc.st_off[PH], alpha);   // log-MAP only
         gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
@@ -943,7 +969,7 @@ struct AlphaSchedS {
 #ifdef TD_DIAG_SPARSE_ASCHED   // diagnostics only (wrong log-MAP results): alpha stored at phase 0 only
             if constexpr (PH == 0)
 #endif
-            astore_row<T, K>(sa, va[PH], alpha, arow);
+            if constexpr ((kCkPh<ALGO> >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
@@ -952,7 +978,7 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr ((kCkPhases >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
+            if constexpr ((kCkPh<ALGO> >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
@@ -1210,17 +1236,18 @@ __device__ __forceinline__ T fold8(const T* v, const T* lut)
     return t;
 }
 
-// Max-Log-MAP alpha step in one lane, all 8 states (:975-1001 with f = 0): the alpha wave's
-// arithmetic exactly -- each state's two candidates alpha[p] -+ (P|Q) (fma(+-1, G, alpha) there),
-// their max, the max over the states (tempmax, exact in any order) and the subtraction.
-template <typename T>
-__device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q)
+// Alpha step in one lane, all 8 states (:975-1001): the alpha wave's arithmetic exactly -- each
+// state's two candidates alpha[p] -+ (P|Q) (fma(+-1, G, alpha) there), their max* (symmetric: the
+// table reads |d|, so the operands may come in either order; Max-Log-MAP: the max), the max over
+// the states (tempmax, exact in any order) and the subtraction.
+template <typename T, int ALGO>
+__device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q, const T* lut)
 {
     T n[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
-        n[j] = vmax(a[p0] - (kTrellisQ[p0] ? Q : P), a[p1] + (kTrellisQ[p1] ? Q : P));
+        n[j] = mstar<T, ALGO>(a[p0] - (kTrellisQ[p0] ? Q : P), a[p1] + (kTrellisQ[p1] ? Q : P), lut);
     }
     const T m = vmax(vmax(vmax(n[0], n[1]), vmax(n[2], n[3])), vmax(vmax(n[4], n[5]), vmax(n[6], n[7])));
 #pragma unroll
@@ -1244,16 +1271,16 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     T a[8], b[8], t0[8], t1[8];
     const T* bv = &sm.Bv[t & 1][k][c * 8];
     load_block<T>(bv, k, b);
-    if constexpr (ALGO == 1) {
+    if constexpr (!kCkAll<ALGO>) {
         // alpha[.][i] from the last stored step ks <= k, recomputed through the steps in between
         // exactly as the alpha wave computed them (:975-1001)
         int ks;
-        const int r = ck_row_of(k, ks);
+        const int r = ck_row_of<ALGO>(k, ks);
         const T* av = &sm.Av[t % kAvSlots][r][c * 8];
         load_block<T>(av, av_rot<ALGO>(r, c), a);
         for (int s = ks; s < k; ++s) {
             const T* gs = &sm.G[t % 3][s][c][0];
-            alpha_recompute<T>(a, gs[0], gs[1]);
+            alpha_recompute<T, ALGO>(a, gs[0], gs[1], lut);
         }
     } else {
         const T* av = &sm.Av[t % kAvSlots][k][c * 8];
@@ -1308,7 +1335,10 @@ struct FoldLane {
     const T* G;      // &sm.G[0][k][c][0]
     const int* Wp;   // &sm.Wp[0][k][c][0]
     const T* Bv;     // &sm.Bv[0][k][c * 8]
-    const T* Av;     // &sm.Av[0][k][c * 8]
+    const T* Av;     // &sm.Av[0][r][c * 8], r = the stored row of step k (or the one before it)
+    int arot;        // the block rotation of that row (av_rot)
+    int rec;         // steps recomputed from the stored row (0 when every row is kept)
+    const T* Gr;     // &sm.G[0][k - rec][c][0]: the recomputed steps' (P, Q)
     T* ext;          // this codeword's extrinsic row base
     uint8_t* bits;   // this codeword's decision row (nullptr: none)
 };
@@ -1323,7 +1353,11 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const int wperm = wp[0], wbit = wp[1];
     T a[8], b[8], t0[8], t1[8];
     load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
-    load_block<T>(fl.Av + s4 * (kW * kLanes), k, a);
+    load_block<T>(fl.Av + s4 * (kW * kLanes), kCkAll<ALGO> ? k : fl.arot, a);
+    if constexpr (!kCkAll<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
+        const T* gr = fl.Gr + s3 * (kW * kCw * 4);
+        for (int q = 0; q < fl.rec; ++q) alpha_recompute<T, ALGO>(a, gr[q * kCw * 4], gr[q * kCw * 4 + 1], lut);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
@@ -1664,13 +1698,15 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
         int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
-        if constexpr (ALGO == 1 && TD_ML_FOLD_MAP && kCkPhases == 1) {
-            // Max-Log-MAP items by recompute depth (alpha stored at k = 0 mod 3): the fold wave
-            // beside the other workgroup's beta (F1) takes the steps k = 0, 1 mod 3 (64 items, at
-            // most one recomputed step), wave A (beside the loader) the steps k = 2 mod 3 (32 items,
-            // two).  With items in step order every wave paid two recomputed steps.
+        if constexpr (!kCkAll<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP)) {
+            // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
+            // takes the 32 items of the phase furthest from a kept row (pd), the fold wave beside
+            // the other workgroup's beta (F1) the 64 items of the other two phases.  Max-Log-MAP
+            // keeping phase 0: A recomputes two steps, F1 at most one; with items in step order
+            // every wave paid two (+0.4 %, config 3).
+            constexpr int pd = kCkDeepest<ALGO>, pa = pd == 0 ? 1 : 0, pb = pd == 2 ? 1 : 2;
             const int q = lane >> 3;
-            fe = wave == 0 ? (3 * q + 2) * kCw + (lane & 7) : (3 * (q >> 1) + (q & 1)) * kCw + (lane & 7);
+            fe = wave == 0 ? (3 * q + pd) * kCw + (lane & 7) : (3 * (q >> 1) + ((q & 1) ? pb : pa)) * kCw + (lane & 7);
             nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
         }
         int j0 = 0;
@@ -1695,7 +1731,16 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             fl.G = &sm.G[0][ke][fl.c][0];
             fl.Wp = &sm.Wp[0][ke][fl.c][0];
             fl.Bv = &sm.Bv[0][ke][fl.c * 8];
-            fl.Av = &sm.Av[0][ke][fl.c * 8];
+            if constexpr (kCkAll<ALGO>) {
+                fl.Av = &sm.Av[0][ke][fl.c * 8];
+            } else {
+                int ks;
+                const int r = ck_row_of<ALGO>(ke, ks);
+                fl.Av = &sm.Av[0][r][fl.c * 8];
+                fl.arot = av_rot<ALGO>(r, fl.c);
+                fl.rec = ke - ks;
+                fl.Gr = &sm.G[0][ks][fl.c][0];
+            }
             fl.ext = dst.ext + (size_t)gm.g * dst.ext_len * kCw + fl.c;
             const int b_ = gm.g * kCw + fl.c;
             fl.bits = (dst.bits && b_ < gm.B) ? dst.bits + (size_t)b_ * dst.bits_stride + (size_t)dst.bits_row * gm.K
