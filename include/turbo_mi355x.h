@@ -134,6 +134,9 @@ int td_debug_stamp_slots(void);
  * candidate workspaces timed (0 = plain allocation), their probe times in ms (up to cap of them)
  * and the index kept. */
 int td_debug_placement(td_handle* h, float* ms, int cap, int* pick);
+/* The placement search's stop rule on probe times ms[0..n) (host only, for tests): 1 if the search
+ * would stop after them (the fast mode seen), else 0; TD_EINVAL on a bad argument. */
+int td_debug_placement_rule(const float* ms, int n);
 
 /* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
  *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)

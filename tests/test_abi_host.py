@@ -242,3 +242,19 @@ def test_multi_gpu_example_builds(tmp_path):
                            f"-Wl,-rpath,{pkg}", "-Wl,-rpath,/opt/rocm/lib", "-o", out])
     r = subprocess.run([out], capture_output=True, text=True)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+@pytest.mark.parametrize("ms,stop", [
+    ([2.3898, 2.3797, 2.3829, 2.378, 2.3972, 2.3827, 2.4883], 0),   # round 2's driver box: all slow + a straggler
+    ([2.3898, 2.3797], 0),                                          # two candidates never decide
+    ([2.3898, 2.3797, 2.2212], 1),                                  # a fast one below the median
+    ([2.2812, 2.3907, 2.4039], 1),                                  # fast first, then two slow
+    ([2.2895, 2.2386, 2.2215, 2.2343, 2.2303], 0),                  # fast mode only: keep looking
+    ([2.2895, 2.2386, 2.2215, 2.2343, 2.3797, 2.4022, 2.3166], 1),  # ... until the slow mode shows thrice
+])
+def test_placement_stop_rule(ms, stop):
+    """td_reserve's placement search stops only once the fast mode is evident (td_api.cpp
+    placement_fast_seen): never on a slow straggler."""
+    import ctypes as C
+    arr = (C.c_float * len(ms))(*ms)
+    assert N.lib().td_debug_placement_rule(arr, len(ms)) == stop

@@ -1,0 +1,70 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (GPU sanitizers
+are not available, so only host code is instrumented):
+  * the C ABI's host paths (tests/host_abi_sanitize.cpp, linked with the library sources built by
+    hipcc with -fsanitize on the host side only): tables, max* table, rand() jump-ahead, the
+    placement stop rule, every entry point's argument checks;
+  * the CPU checker (oracle/turbo_oracle.c via tests/oracle_sanitize.c): threaded batch decodes,
+    both algorithms and precisions; its decisions equal the uninstrumented liboracle.so's."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+CSRC = os.path.join(REPO, "turbo_decoder_cuda_amd", "csrc")
+SAN = ["-fsanitize=address", "-fsanitize=undefined", "-fno-sanitize-recover=undefined"]
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+
+
+def _run(exe):
+    r = subprocess.run([exe], capture_output=True, text=True, env=ENV, timeout=600)
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+    return r
+
+
+@pytest.mark.timeout(600)
+def test_host_abi_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "host_abi_sanitize")
+    hip_san = [a for s in SAN for a in ("-Xarch_host", s)]
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-ffp-contract=off",
+           "-fno-honor-nans", f"-I{REPO}/include", f"-I{CSRC}", *hip_san,
+           os.path.join(REPO, "tests", "host_abi_sanitize.cpp"), os.path.join(CSRC, "td_api.cpp"),
+           os.path.join(CSRC, "td_kernels.hip"), os.path.join(CSRC, "td_synth.hip"), "-o", exe]
+    subprocess.check_call(cmd)
+    r = _run(exe)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "0 failed checks" in r.stdout
+
+
+def test_oracle_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "oracle_sanitize")
+    odir = os.path.join(REPO, "oracle")
+    subprocess.check_call(["gcc", "-O1", "-g", "-std=c11", "-ffp-contract=off", *SAN, f"-I{odir}",
+                           os.path.join(REPO, "tests", "oracle_sanitize.c"), os.path.join(odir, "turbo_oracle.c"),
+                           "-lm", "-lpthread", "-o", exe])
+    r = _run(exe)
+    assert r.returncode == 0, r.stderr[-4000:]
+    # the same decodes through the uninstrumented checker
+    import pyoracle as O
+    lib = O.lib()
+    lib.tdo_synth_batch.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p]
+    lib.tdo_decode_batch.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                     C.c_void_p, C.c_int]
+    s = 0
+    for K, f1, f2, k in ((40, 3, 10, 0), (1024, 31, 64, 1)):
+        B, n = 5, 3 * K + 12
+        src = np.zeros(B * K, dtype=np.int32)
+        flow = np.zeros(B * n, dtype=np.float64)
+        lib.tdo_synth_batch(K, f1, f2, 0.4, 77 + k, B, src.ctypes.data, flow.ctypes.data)
+        flow32 = flow.astype(np.float32)
+        for algo in (0, 1):
+            for f32 in (0, 1):
+                bits = np.zeros(B * K, dtype=np.uint8)
+                x = flow32 if f32 else flow
+                lib.tdo_decode_batch(K, f1, f2, 3, algo, f32, x.ctypes.data, B, bits.ctypes.data, 2)
+                for v in bits:
+                    s = (s * 1000003 + int(v)) % (1 << 64)
+    assert int(r.stdout.strip()) == s

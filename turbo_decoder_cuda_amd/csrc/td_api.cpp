@@ -962,6 +962,12 @@ int td_debug_swap_arrays(td_handle* a, td_handle* b, int mask)
 }
 #endif
 
+int td_debug_placement_rule(const float* ms, int n)
+{
+    if (!ms || n < 0) return fail(TD_EINVAL, "td_debug_placement_rule: bad argument");
+    return placement_fast_seen(std::vector<float>(ms, ms + n)) ? 1 : 0;
+}
+
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
