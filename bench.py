@@ -231,6 +231,29 @@ def traffic_model(K: int, B: int, iters: int, esz: int, algo: str) -> dict:
             "scratch_share": round((alpha + tm) / total, 4)}
 
 
+# Dependent-chain cycles per trellis step of the two recursions, each alone on a SIMD with its
+# operands in registers (scripts/ubench_alpha.hip, scripts/ubench_beta.hip): fp64
+# log-MAP alpha 200 (218 with its two scratch stores), beta 148.
+CHAIN_CYCLES_F64_LOGMAP = {"alpha": 218, "beta": 148}
+SCLK_GHZ = 2.35   # the kernel's sustained shader clock on MI355X (s_memtime vs s_memrealtime)
+
+
+def latency_floor(a, turbo_ms):
+    """The exact schedule's own speed of light: every codeword of a dispatch round is in flight at
+    once, so a launch cannot beat 2*iters SISOs x L steps x (alpha step + beta step), the two serial
+    recursions back to back, at the chains' isolated per-step latency.  frac = floor / measured."""
+    if a.window or a.algo != "logmap" or a.precision != "f64" or turbo_ms <= 0:
+        return None
+    rounds = -(-((a.batch + 7) // 8) // 512)   # dispatch rounds of 512 workgroups (2 per CU)
+    cyc = CHAIN_CYCLES_F64_LOGMAP["alpha"] + CHAIN_CYCLES_F64_LOGMAP["beta"]
+    floor_ms = rounds * 2 * a.iters * (a.K + 3) * cyc / (SCLK_GHZ * 1e9) * 1e3
+    return {"floor_ms": round(floor_ms, 3), "frac": round(floor_ms / turbo_ms, 4),
+            "chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP, "sclk_ghz": SCLK_GHZ, "dispatch_rounds": rounds,
+            "note": "serial alpha + beta chains at their isolated per-step latency (microbenchmarks), "
+                    "the bound this latency-limited kernel is measured against; the HBM fraction above "
+                    "is the metric's contract"}
+
+
 def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2) -> dict:
     """The bench JSON record.  value = info bits decoded by ALL ranks / max-over-ranks time."""
     ms_step = elapsed / a.steps * 1e3
@@ -301,6 +324,7 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
             "traffic_frac_measured_ceiling": round(traffic_gbs / HBM_MEASURED_GBS, 4) if traffic_gbs else None,
             "measured_ceiling_gbs": HBM_MEASURED_GBS,
             "traffic_model": model,
+            "latency_floor": latency_floor(a, turbo_ms),
             "limiter": ("latency of the serial alpha / beta recursions (one dependent trellis step at a time "
                         "per codeword; DESIGN.md 3.2): neither HBM nor VALU is saturated") if not a.window else
                        "VALU / LDS issue of the sub-block chains (DESIGN.md 8.3)",
