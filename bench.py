@@ -129,6 +129,8 @@ def main():
     f1, f2 = qpp_for(a.K)
     first, a.batch = shard_layout(world, rank, per_gpu_batch(a, world), a.strong, a.global_batch)
     a.total = a.global_batch if a.strong else a.batch * world
+    if a.batch < 1:
+        raise SystemExit(f"bench: rank {rank} has no codewords (--global-batch {a.global_batch} < {world} ranks)")
 
     codec = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=a.algo, precision=a.precision, device=local)
     # this rank's slice of the global frame stream: frames [first, first + batch) of srand(SEED)
