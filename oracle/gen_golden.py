@@ -37,6 +37,11 @@ FRAME_CASES = [
     (6144, 263, 480, 0.3, 21, 1, 8, np.float32),
     (6144, 263, 480, 1.0, 21, 1, 8, np.float32),
     (40, 3, 10, 0.0, 31, 4, 8, np.float64),      # smallest LTE QPP size (36.212 Table 5.1.3-3)
+    # round 3: trellis lengths below one kernel window (L = 11) and at the reference's capacity
+    # (MAX_FRAME_LENGTH 10000, log_map.h:31), with QPP parameters that give permutations there
+    (8, 1, 2, 0.5, 41, 2, 4, np.float64),
+    (24, 1, 6, 0.5, 42, 2, 4, np.float64),
+    (10000, 1, 10, 0.8, 43, 1, 4, np.float32),
 ]
 
 

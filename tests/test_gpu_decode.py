@@ -213,3 +213,19 @@ def test_one_handle_two_streams():
     for f, b in zip(flows, outs):
         ob = O.decode_batch(np.ascontiguousarray(f), K, f1, f2, iters, nthreads=4)
         assert np.array_equal(b.cpu().numpy(), ob)
+
+
+@pytest.mark.parametrize("K,f1,f2", [(1, 1, 2), (5, 1, 10), (16, 1, 4)])
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+def test_tiny_K_vs_oracle(K, f1, f2, algo):
+    """Trellises shorter than one 12-step kernel window (L = 4, 8) and one window and a half
+    (L = 19): every iteration's bits equal the oracle's, Le within 1e-9 (the reference's own
+    frames at K = 8, 24 and 10000 are in tests/golden and run through test_turbo_vs_reference)."""
+    B, iters = 9, 3
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 700 + K, B)
+    bits, le = _decode_all(K, f1, f2, iters, flow, algo=algo)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(B):
+        ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
+        assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
+        assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
