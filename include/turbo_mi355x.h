@@ -71,7 +71,7 @@ int td_reserve(td_handle* h, int B);
  * 1 = a plain allocation); the search stops once one candidate runs >= 4 % below the median of
  * those timed (at least three), never on a slow straggler.  Transient memory: every candidate is
  * held until the choice (so each gets fresh pages), at most half the free device memory and at
- * most 96 GiB in total (config 2: ~2.4 GiB a candidate; a 32768-codeword batch: ~19 GiB).
+ * most 144 GiB in total (config 2: ~2.4 GiB a candidate; a 32768-codeword batch: ~19 GiB).
  * Results do not depend on it. */
 
 /*

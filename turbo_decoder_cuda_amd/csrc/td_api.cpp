@@ -353,10 +353,11 @@ bool placement_fast_seen(const std::vector<float>& ms)
 }
 
 // Candidate workspaces the search may hold at once: half the free device memory, and at most
-// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  96 GiB
-// lets config 4's 32768-codeword shard (19 GiB a workspace) try five candidates: with two (the
-// 48 GiB cap of round 3's first runs) both landed in the slow mode (18.96 / 18.58 ms probes).
-constexpr size_t kPlaceHoldBytes = (size_t)96 << 30;
+// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  144 GiB
+// lets config 4's 32768-codeword shard (19 GiB a workspace) try seven candidates: with two (the
+// 48 GiB cap of round 3's first runs) both landed in the slow mode (18.96 / 18.58 ms probes), and
+// at N = 8 the slowest of eight ranks sets the step time, so every rank should find the fast mode.
+constexpr size_t kPlaceHoldBytes = (size_t)144 << 30;
 
 int place_ws(td_handle* h, int G)
 {
