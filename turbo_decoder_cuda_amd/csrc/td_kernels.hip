@@ -111,6 +111,34 @@ __device__ __forceinline__ T group_max8(T v)
     return v;
 }
 
+// The alpha step's tempmax (the max over the codeword's 8 lanes) and the partner's metric an.
+// TD_QMAX=1: the three quad mates are read in one DPP level (quad_perm xor 1, 2, 3), their max is
+// a two-deep tree, and one row_half_mirror of it brings the other quad's: DPP, max, max, DPP, max
+// on the chain instead of three (DPP, max) levels, for two more VALU ops (and, at phase 2, the
+// partner's mirror beside the tree).  Exact in any order.  Measured slower on one box (2 interleaved
+// rounds, B=4096): fp64 log-MAP 17.51 -> 17.80 ms, fp64 max-log 11.56 -> 11.74, fp32 max-log 10.36 ->
+// 10.56; fp32 log-MAP 15.17 -> 15.10.  In fp64 the DPP pairs' issue, not their hazard, is the cost,
+// and the tree issues the same movs ahead of its first max.  Default off.
+#ifndef TD_QMAX
+#define TD_QMAX 0
+#endif
+constexpr int kDppXor3 = 0x1B;    // quad_perm [3,2,1,0]
+template <typename T, int PH>
+__device__ __forceinline__ T alpha_tempmax(T a, T& an)
+{
+    if constexpr (TD_QMAX != 0) {
+        const T x1 = dpp<kDppXor1>(a), x2 = dpp<kDppXor2>(a), x3 = dpp<kDppXor3>(a);
+        const T q = vmax(vmax(a, x1), vmax(x2, x3));
+        an = PH == 0 ? x1 : (PH == 1 ? x2 : dpp<kDppMir8>(a));
+        return vmax(q, dpp<kDppMir8>(q));
+    } else {
+        an = dpp<PhaseDpp<PH>::ctrl>(a);
+        T m = vmax(a, an);
+        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+        return vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
+    }
+}
+
 // ------------------------------------------------------------------ max*
 // Exact bucket form of E_algorithm (td_tables.h, build_lut): the bucket index is a bit field of
 // d (exponent + 2 mantissa bits; the sign bit is outside the field, so d need not be |d|).
@@ -717,10 +745,8 @@ template <typename T, int ALGO, int PH>
 __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc,
                                                    T* pa, T* ptm)
 {
-    const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw
-    T m = vmax(a, an);
-    m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
-    m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
+    T an;                                         // partner's alpha_raw
+    const T m = alpha_tempmax<T, PH>(a, an);       // tempmax[i] (:986-993)
     const T alpha = a - m, ap = an - m;             // alpha[.][i] of this lane and of the partner
     StepHalf<T> h;
     h.xs = fma(lc.a_sg[PH], in.gs, alpha);   // gamma + alpha, predecessor in this lane
@@ -855,10 +881,8 @@ struct AlphaSched {
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
-        const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw (first level of the max)
-        T m = vmax(a, an);
-        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
-        m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));   // tempmax[i] (:986-993)
+        T an;                                         // partner's alpha_raw
+        const T m = alpha_tempmax<T, PH>(a, an);       // tempmax[i] (:986-993)
         const T alpha = a - m, ap = an - m;                   // :995-1000
         const T xs = fma(lc.a_sg[PH], in.gs, alpha);
         const T xp = fma(lc.a_pg[PH], in.gp, ap);
@@ -951,10 +975,8 @@ struct AlphaSchedS {
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
-        const T an = dpp<PhaseDpp<PH>::ctrl>(a);
-        T m = vmax(a, an);
-        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
-        m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));   // tempmax[i] (:986-993)
+        T an;                                         // partner's alpha_raw
+        const T m = alpha_tempmax<T, PH>(a, an);       // tempmax[i] (:986-993)
         const T alpha = a - m, ap = an - m;                   // :995-1000
         const T xs = fma(lc.a_sg[PH], in.gs, alpha);
         const T xp = fma(lc.a_pg[PH], in.gp, ap);
