@@ -80,6 +80,25 @@ def test_maxlog_vs_oracle(precision):
         assert np.abs(le[b] - ol).max() <= tol * max(1.0, np.abs(ol).max() if precision == "f32" else 1.0)
 
 
+def test_f32_maxlog_three_workgroups_per_cu(monkeypatch):
+    """B = 6150 in fp32 Max-Log-MAP is 769 codeword groups, more than two per CU, so the decode
+    runs turbo_decode_kernel3 (three workgroups per CU).  Its bits and Le equal the two-workgroup
+    kernel's (TD_OCC3=0) exactly, and a sample of codewords equals the oracle."""
+    K, f1, f2, B, iters = 40, 3, 10, 6150, 3
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 31, B)
+    flow = flow.astype(np.float32)
+    monkeypatch.setenv("TD_OCC3", "0")
+    bits2, le2 = _decode_all(K, f1, f2, iters, flow, algo="maxlog", precision="f32")
+    monkeypatch.setenv("TD_OCC3", "1")
+    bits3, le3 = _decode_all(K, f1, f2, iters, flow, algo="maxlog", precision="f32")
+    assert np.array_equal(bits2, bits3)
+    assert np.array_equal(le2.view(np.uint32), le3.view(np.uint32))
+    for b in range(0, B, 307):
+        ob, ol = O.turbo_decode(flow[b].astype(np.float64), K, f1, f2, iters, algo=O.ALGO_MAXLOG)
+        assert np.array_equal(bits3[b], ob.astype(np.uint8)), f"codeword {b}"
+        assert np.abs(le3[b] - ol).max() <= 2e-3 * max(1.0, np.abs(ol).max()), f"codeword {b}"
+
+
 def test_f32_logmap_vs_oracle_f32():
     """fp32 throughput mode against the oracle's fp32 restatement (same op order): bits identical
     on converged frames, Le close relative to its magnitude."""

@@ -80,6 +80,7 @@ struct td_handle {
     int win_cap = 0;
     int modulation = 1;                          // td_synth_modulation (MODULATION)
     int role_cus = 0;                            // CU count for the kernel's role rotation (wg_pos)
+    int occ3 = 1;                                // TD_OCC3=0: never three workgroups per CU
     // decoding schedule (td_set_window): window 0 = exact full trellis
     td::WindowParams wp{0, 0, 0, 0, 1.0f};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
@@ -155,6 +156,7 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
     dp.algo = h->p.algo;
     dp.role_cus = h->role_cus;
+    dp.occ3 = h->occ3;
     dp.cu_slots = h->d_slots;
 }
 
@@ -765,6 +767,8 @@ int td_create(td_handle** out, const td_params* p)
     {
         const char* rot = std::getenv("TD_ROLE_ROT");   // diagnostics: 0 disables the role rotation
         h->role_cus = (rot && std::atoi(rot) == 0) ? 0 : prop.multiProcessorCount;
+        const char* o3 = std::getenv("TD_OCC3");      // 0: large batches stay on two workgroups per CU
+        h->occ3 = (o3 && std::atoi(o3) == 0) ? 0 : 1;
     }
     {
         td::LutEntry<double> l64[td::kLutSize];

@@ -85,6 +85,7 @@ struct DecodeParams {
     unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
     int K, L, nT, G, B, iters, all_iters, algo;
     int role_cus;               // CU count for the second-round role rotation (wg_pos); 0 = off
+    int occ3;                   // 1: large batches on three workgroups per CU where built (turbo_decode_kernel3)
     int sys2_in_turbo;          // 1: the turbo kernel forms sys2 = sys1 o pi itself (first SISO's F pass),
                                 // launch_demux skips demux_perm_kernel (exact schedule only)
     unsigned* cu_slots;         // [kCuSlotKeys] per-CU occupancy bits (placement-based roles, wg_pos)

@@ -1865,7 +1865,7 @@ struct WgPos {
 // shares only with a loader, the two fold waves sharing the remaining SIMDs.
 //
 // TD_ROLE_MAP 2 (default) makes the pairing independent of the dispatcher: the waves read their
-// SIMD from HW_ID and the workgroup takes a free slot (0 or 1) of its CU in a per-CU occupancy
+// SIMD from HW_ID and the workgroup takes a free slot (0 or 1; 2 for turbo_decode_kernel3) of its CU in a per-CU occupancy
 // word (atomicOr; released at the end, wg_release); role = SIMD for slot 0 and SIMD ^ 2 for slot
 // 1, which gives the pairs A/F0, B/F1 on every SIMD whatever order the workgroups arrived in
 // (a preceding kernel with many small blocks shifted the round-based placement: +4 % kernel time).
@@ -1890,8 +1890,8 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
         const int simd = (int)((hw >> 4) & 3);
         const int key = (int)((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
         if (threadIdx.x == 0) {
-            int slot = 0;
-            if (atomicOr(&slots[key], 1u) & 1u) slot = (atomicOr(&slots[key], 2u) & 2u) ? 2 : 1;
+            int slot = 0;   // the first free of slots 0..2 (3: none)
+            while (slot < 3 && (atomicOr(&slots[key], 1u << slot) & (1u << slot))) ++slot;
             s_slot = slot;
         }
         if (lane == 0) s_simd[wave] = simd;
@@ -1903,7 +1903,9 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
             for (int b = a + 1; b < kWaves; ++b) distinct = distinct && s_simd[a] != s_simd[b];
         const int slot = s_slot;
         const int base = distinct ? simd : wave;
-        return WgPos{h, slot == 1 ? base ^ TD_SLOT_XOR : base, lane, g, key, slot};
+        // slot 2 (turbo_decode_kernel3's third workgroup): role = SIMD ^ 1, so that the three
+        // workgroups' alpha chains (and their beta chains) sit on three different SIMDs
+        return WgPos{h, slot == 1 ? base ^ TD_SLOT_XOR : (slot == 2 ? base ^ 1 : base), lane, g, key, slot};
     }
     const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
     int role;
@@ -1920,7 +1922,7 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
 // end of the kernel: give the CU slot back (all waves of the workgroup are past their work)
 __device__ __forceinline__ void wg_release(const WgPos& w, unsigned* slots)
 {
-    if (w.slot < 2) {
+    if (w.slot < 3) {
         __syncthreads();
         if (threadIdx.x == 0) atomicAnd(&slots[w.slot_key], ~(1u << w.slot));
     }
@@ -1980,6 +1982,24 @@ template <typename T, int ALGO>
 __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
 {
     turbo_decode_body<T, ALGO>(p);
+}
+
+// Large batches (more groups than two per CU): three workgroups per CU -- 24 codewords, 12 waves,
+// three per SIMD -- where the build fits them: at most 168 VGPRs without scratch and a third of
+// the CU's LDS.  fp32 Max-Log-MAP fits as it is (143 VGPRs, 42 KB); fp32 log-MAP needs 191 and
+// fp64 240-256 (TD_OCC3_F32LOG builds the fp32 log-MAP one anyway, for the resource report).
+#ifndef TD_OCC3
+#define TD_OCC3 1
+#endif
+#ifndef TD_OCC3_F32LOG
+#define TD_OCC3_F32LOG 0
+#endif
+template <typename T, int ALGO>
+constexpr bool kOcc3 = TD_OCC3 != 0 && kGroupsPerWg == 1 && sizeof(T) == 4 && (ALGO == 1 || TD_OCC3_F32LOG != 0);
+template <typename T, int ALGO>
+__global__ __launch_bounds__(kWaves * 64, 3) void turbo_decode_kernel3(DecodeParams<T> p)
+{
+    if constexpr (kOcc3<T, ALGO>) turbo_decode_body<T, ALGO>(p);
 }
 
 // td_reserve's workspace-placement probe (td_api.cpp place_ws): the same code as
@@ -2490,9 +2510,17 @@ constexpr size_t wg_lds()
 }
 static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
 
+static_assert(3 * (sizeof(Smem<float>) + 64) <= 160 * 1024, "three fp32 workgroups per CU");
+
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool probe)
 {
+    if (kOcc3<T, ALGO> && !probe && p.occ3 && p.role_cus > 0 && p.G > 2 * p.role_cus) {
+        hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel3<T, ALGO>), sizeof(Smem<T>));
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((turbo_decode_kernel3<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
+        return hipGetLastError();
+    }
     const void* k = probe ? reinterpret_cast<const void*>(&turbo_placement_probe_kernel<T, ALGO>)
                           : reinterpret_cast<const void*>(&turbo_decode_kernel<T, ALGO>);
     hipError_t e = allow_smem(k, wg_lds<T>());
