@@ -80,23 +80,56 @@ def test_maxlog_vs_oracle(precision):
         assert np.abs(le[b] - ol).max() <= tol * max(1.0, np.abs(ol).max() if precision == "f32" else 1.0)
 
 
-def test_f32_maxlog_three_workgroups_per_cu(monkeypatch):
-    """B = 6150 in fp32 Max-Log-MAP is 769 codeword groups, more than two per CU, so the decode
-    runs turbo_decode_kernel3 (three workgroups per CU).  Its bits and Le equal the two-workgroup
-    kernel's (TD_OCC3=0) exactly, and a sample of codewords equals the oracle."""
-    K, f1, f2, B, iters = 40, 3, 10, 6150, 3
-    _, flow = O.synth_batch(K, f1, f2, 0.3, 31, B)
-    flow = flow.astype(np.float32)
+def _decode_bits(K, f1, f2, iters, flow, algo="logmap", precision="f64"):
+    """Every iteration's bits without an Le dump: the folds' fast path (siso_wg, TD_FOLD_FAST)."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    dt = torch.float64 if precision == "f64" else torch.float32
+    x = torch.from_numpy(flow).to(_dev()).to(dt).contiguous()
+    with TurboCodec(K, f1, f2, iterations=iters, algo=algo, precision=precision) as c:
+        bits = torch.empty((flow.shape[0], iters, K), dtype=torch.uint8, device=x.device)
+        c.decode(x, bits, all_iters=True)
+        torch.cuda.synchronize()
+    return bits.cpu().numpy()
+
+
+@pytest.mark.parametrize("precision,algo,K,f1,f2", [("f32", "maxlog", 40, 3, 10), ("f32", "logmap", 40, 3, 10),
+                                                    ("f64", "maxlog", 40, 3, 10), ("f64", "logmap", 40, 3, 10),
+                                                    ("f64", "logmap", 1024, 31, 64)])
+def test_three_workgroups_per_cu(monkeypatch, precision, algo, K, f1, f2):
+    """B = 6150 is 769 codeword groups, more than two per CU, so the decode runs
+    turbo_decode_kernel3 (three workgroups per CU) where the build has it.  Its bits and Le equal
+    the two-workgroup kernel's (TD_OCC3=0) exactly -- with an Le dump (the generic fold) and
+    without (the fast fold) -- and a sample of codewords matches the oracle: fp64 bit for bit
+    (Le to 1e-9); fp32 as test_maxlog_vs_oracle / test_f32_logmap_vs_oracle_f32 (log-MAP: the
+    last iteration's bits on converged frames at 1.0 dB)."""
+    B, iters = 6150, 3
+    _, flow = O.synth_batch(K, f1, f2, 0.3 if (algo == "maxlog" or precision == "f64") else 1.0, 31, B)
+    if precision == "f32":
+        flow = flow.astype(np.float32)
     monkeypatch.setenv("TD_OCC3", "0")
-    bits2, le2 = _decode_all(K, f1, f2, iters, flow, algo="maxlog", precision="f32")
+    bits2, le2 = _decode_all(K, f1, f2, iters, flow, algo=algo, precision=precision)
+    fast2 = _decode_bits(K, f1, f2, iters, flow, algo=algo, precision=precision)
     monkeypatch.setenv("TD_OCC3", "1")
-    bits3, le3 = _decode_all(K, f1, f2, iters, flow, algo="maxlog", precision="f32")
+    bits3, le3 = _decode_all(K, f1, f2, iters, flow, algo=algo, precision=precision)
+    fast3 = _decode_bits(K, f1, f2, iters, flow, algo=algo, precision=precision)
     assert np.array_equal(bits2, bits3)
-    assert np.array_equal(le2.view(np.uint32), le3.view(np.uint32))
-    for b in range(0, B, 307):
-        ob, ol = O.turbo_decode(flow[b].astype(np.float64), K, f1, f2, iters, algo=O.ALGO_MAXLOG)
-        assert np.array_equal(bits3[b], ob.astype(np.uint8)), f"codeword {b}"
-        assert np.abs(le3[b] - ol).max() <= 2e-3 * max(1.0, np.abs(ol).max()), f"codeword {b}"
+    assert np.array_equal(le2.view(np.uint8), le3.view(np.uint8))
+    assert np.array_equal(fast2, fast3) and np.array_equal(fast3, bits3)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(0, B, 307 if K == 40 else 1201):
+        ob, ol = O.turbo_decode(np.asarray(flow[b], dtype=np.float64), K, f1, f2, iters, algo=oalgo)
+        if precision == "f64":
+            assert np.array_equal(bits3[b], ob.astype(np.uint8)), f"codeword {b}"
+            assert np.abs(le3[b] - ol).max() <= 1e-9, f"codeword {b}"
+            continue
+        if algo == "maxlog":
+            assert np.array_equal(bits3[b], ob.astype(np.uint8)), f"codeword {b}"
+        else:
+            assert np.array_equal(bits3[b, -1], ob[-1].astype(np.uint8)), f"codeword {b}"
+        tol = 2e-3 if algo == "maxlog" else 1e-3
+        assert np.abs(le3[b] - ol).max() <= tol * max(1.0, np.abs(ol).max()), f"codeword {b}"
 
 
 def test_f32_logmap_vs_oracle_f32():

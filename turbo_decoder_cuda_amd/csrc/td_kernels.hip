@@ -305,6 +305,14 @@ constexpr int kFoldA = ALGO == 0 ? TD_FOLD_A : kFoldPerWave;
 #endif
 static_assert(TD_FOLD_A <= kLanes && kTile - TD_FOLD_A <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
+// TD_AV_DIRECT: the fold lanes load their alpha blocks (8 states, 64 B in fp64) from the HBM scratch
+// into registers one window ahead, instead of the loader copying whole windows into an LDS ring
+// (Av): the ring is 24.6 KB of the fp64 workgroup's 69.9 KB of LDS, without it three workgroups fit
+// a CU (turbo_decode_kernel3).  Same bytes from HBM; no alpha LDS writes or reads.
+#ifndef TD_AV_DIRECT
+#define TD_AV_DIRECT 0
+#endif
+constexpr bool kAvDirect = TD_AV_DIRECT != 0;
 
 // Loader staging.  Window inputs travel HBM -> LDS by DMA (global_load_lds_dwordx4: no VGPR
 // destination, completion counted by vmcnt; LDS target = wave-uniform base + 16 * lane) and the
@@ -324,7 +332,8 @@ struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
-    T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
+    T Av[kAvDirect ? 1 : kAvSlots][kAvDirect ? 1 : kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state
+                                                                    // (fold input, DMA from HBM; unused: TD_AV_DIRECT)
     T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
     alignas(16) unsigned char stage[3][kTileDma<T> * kDmaBytes];   // loader: staged window inputs
@@ -654,7 +663,7 @@ __device__ __forceinline__ int ck_row_of(int k, int& ks)
 template <typename T, int ALGO>
 constexpr int alpha_dma_count()
 {
-    return kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
+    return kAvDirect ? 0 : kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
 }
 static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
@@ -1276,6 +1285,25 @@ __device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q, const T* lu
     for (int j = 0; j < 8; ++j) a[j] = n[j] - m;
 }
 
+// TD_AV_DIRECT: the alpha block of (window t, row r, codeword c) in the HBM scratch, and its 8
+// states loaded into registers (one 16-byte load per chunk; the scratch rows are by 8c + state)
+template <typename T>
+__device__ __forceinline__ const T* av_global(const T* astore, const Geom& gm, int t, int r, int c)
+{
+    return astore + astore_window_off(gm.g, t, gm.G, gm.L) + (size_t)r * astore_row_stride(gm.G) + c * 8;
+}
+template <typename T>
+__device__ __forceinline__ void load_block_global(const T* p, T (&v)[8])
+{
+    constexpr int E = 16 / (int)sizeof(T);
+    using V = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
+#pragma unroll
+    for (int q = 0; q < kBlkChunks<T>; ++q) {
+        const V x = *reinterpret_cast<const V*>(p + q * E);
+        __builtin_memcpy(&v[q * E], &x, 16);
+    }
+}
+
 // LLR fold + extrinsic + outputs of item e = k*8 + c of window t (:1024-1039, :1234-1264):
 //   temp_u[j] = (gamma[p][i][u] + alpha[p][i]) + beta[j][i+1],  p = laststat[j][u],
 //   LLR = E_seq(temp1) - E_seq(temp0)
@@ -1283,7 +1311,7 @@ __device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q, const T* lu
 // reference's (gamma + alpha) + beta.  Both folds run in the same lane (independent chains).
 template <typename T, int ALGO>
 __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t, int e, const SisoDst<T>& dst,
-                                          const Geom& gm)
+                                          const Geom& gm, const T* astore)
 {
     const int k = e >> 3, c = e & 7;
     const int i = t * kW + k;
@@ -1298,12 +1326,18 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
         // exactly as the alpha wave computed them (:975-1001)
         int ks;
         const int r = ck_row_of<ALGO>(k, ks);
-        const T* av = &sm.Av[t % kAvSlots][r][c * 8];
-        load_block<T>(av, av_rot<ALGO>(r, c), a);
+        if constexpr (kAvDirect) {
+            load_block_global<T>(av_global(astore, gm, t, ks, c), a);   // the scratch keeps rows at their steps
+        } else {
+            const T* av = &sm.Av[t % kAvSlots][r][c * 8];
+            load_block<T>(av, av_rot<ALGO>(r, c), a);
+        }
         for (int s = ks; s < k; ++s) {
             const T* gs = &sm.G[t % 3][s][c][0];
             alpha_recompute<T, ALGO>(a, gs[0], gs[1], lut);
         }
+    } else if constexpr (kAvDirect) {
+        load_block_global<T>(av_global(astore, gm, t, k, c), a);
     } else {
         const T* av = &sm.Av[t % kAvSlots][k][c * 8];
         load_block<T>(av, k, a);
@@ -1366,7 +1400,7 @@ struct FoldLane {
 };
 template <typename T, int ALGO>
 __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* lut, int s3, int s4, int s2, int i0,
-                                               int ext_len, int K)
+                                               int ext_len, int K, const T (&ain)[8])
 {
     const int k = fl.k;
     const T* g = fl.G + s3 * (kW * kCw * 4);
@@ -1375,7 +1409,12 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const int wperm = wp[0], wbit = wp[1];
     T a[8], b[8], t0[8], t1[8];
     load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
-    load_block<T>(fl.Av + s4 * (kW * kLanes), kCkAll<ALGO> ? k : fl.arot, a);
+    if constexpr (kAvDirect) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = ain[j];   // loaded one window ahead (siso_wg)
+    } else {
+        load_block<T>(fl.Av + s4 * (kW * kLanes), kCkAll<ALGO> ? k : fl.arot, a);
+    }
     if constexpr (!kCkAll<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
         const T* gr = fl.Gr + s3 * (kW * kCw * 4);
         for (int q = 0; q < fl.rec; ++q) alpha_recompute<T, ALGO>(a, gr[q * kCw * 4], gr[q * kCw * 4 + 1], lut);
@@ -1392,12 +1431,18 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     for (int j = 2; j < 8; ++j) r0 = mstar<T, ALGO>(r0, t0[j] + t1[j], lut);
     const T r1 = P;
 #else
-    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
-    T r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
+    T r0, r1;
+    if constexpr (ALGO == 1) {   // Max-Log-MAP: a max tree (exact in any order), as fold_item
+        r0 = vmax(vmax(vmax(t0[0], t0[1]), vmax(t0[2], t0[3])), vmax(vmax(t0[4], t0[5]), vmax(t0[6], t0[7])));
+        r1 = vmax(vmax(vmax(t1[0], t1[1]), vmax(t1[2], t1[3])), vmax(vmax(t1[4], t1[5]), vmax(t1[6], t1[7])));
+    } else {
+        r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
+        r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
 #pragma unroll
-    for (int j = 2; j < 8; ++j) {
-        r0 = mstar<T, ALGO>(r0, t0[j], lut);
-        r1 = mstar<T, ALGO>(r1, t1[j], lut);
+        for (int j = 2; j < 8; ++j) {
+            r0 = mstar<T, ALGO>(r0, t0[j], lut);
+            r1 = mstar<T, ALGO>(r1, t1[j], lut);
+        }
     }
 #endif
     const T llr = r1 - r0;
@@ -1418,6 +1463,23 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #ifndef TD_ALPHA_PRIO
 #define TD_ALPHA_PRIO 2   // VALU priority of the alpha wave in the F pass
 #endif
+// TD_LOADER_REMAT: the loader's per-lane DMA addresses are rebuilt in every iteration (the lane index
+// made opaque to the compiler there) instead of being hoisted out of the passes and kept live: the
+// hoisted addresses set the kernel's register count (the loader is the role with the most live VGPRs)
+#ifndef TD_LOADER_REMAT
+#define TD_LOADER_REMAT 0
+#endif
+// TD_ROLE_REMAT: the lane index made opaque at the start of every SISO, so that the compiler cannot
+// hoist the roles' lane-derived addresses (fold lanes, alpha store offsets, ...) out of the SISO loop,
+// where they were all live at once, in every role: fp64 log-MAP 256 -> 95 VGPRs, fp32 log-MAP 191 ->
+// 78, so that three workgroups fit a CU (turbo_decode_kernel3).  1 (default): fp32 only -- at two
+// workgroups per CU it measured level in fp64 log-MAP (17.39 vs 17.40 ms) and 1.4 % slower in fp64
+// Max-Log-MAP; 2: both precisions; 0: off.
+#ifndef TD_ROLE_REMAT
+#define TD_ROLE_REMAT 1
+#endif
+template <typename T>
+constexpr bool kRoleRemat = TD_ROLE_REMAT == 2 || (TD_ROLE_REMAT == 1 && sizeof(T) == 4);
 constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
                                  // barriers, F prologue, loader B prologue, loader first tile (see diag)
@@ -1435,6 +1497,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                         T* tmstore, const LaneTables* lt, int wave, int lane, unsigned long long* st)
 {
     (void)st;
+    if constexpr (kRoleRemat<T>) touch(lane);   // nothing derived from the lane index is SISO-invariant (TD_ROLE_REMAT)
     TD_STAMP(p0);
     const int nT = gm.nT;
     const int tl = nT - 1;
@@ -1530,12 +1593,17 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     } else if (wave == 2) {
         // Loader: every input travels HBM -> LDS by DMA into a staging slot, and this wave converts
         // landed slots into the ring (no VGPR is ever the target of a load in flight).
+        [[maybe_unused]] const int lane_in = lane;
         // Invariant: every iteration ends with a wait that leaves only its own DMAs in flight.
         // F pass iteration t: convert window t+1 (staged two iterations ago, slot (t+1) % 3) and
         // stage window t+3 into slot t % 3, which window t left one iteration ago.
         constexpr int kF = kTileDma<T>;
         auto fstep = [&](int t) {
             TD_STAMP(f0);
+#if TD_LOADER_REMAT
+            int lane = lane_in;   // opaque per iteration: the DMA addresses are rebuilt, not kept live
+            touch(lane);
+#endif
 #ifdef TD_DIAG_NOCONVERT   // diagnostics only (wrong results): the F pass without the loader's LDS
             // traffic but for the last three windows, whose tiles (write positions) the B pass uses
             if (t + 1 <= tl && t + 1 >= tl - 2) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
@@ -1580,6 +1648,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
         auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
+#if TD_LOADER_REMAT
+            int lane = lane_in;
+            touch(lane);
+#endif
             const int wa = tl - j;
             if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
             if (wa >= 0) tm_convert(sm, slot, wa, lane);
@@ -1732,14 +1804,25 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
         }
         int j0 = 0;
-        if (TD_FOLD_FAST && ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
+        if (TD_FOLD_FAST && (ALGO == 0 || kAvDirect) && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
             // here iterations 3 .. nB-1, i.e. the full windows wf = tl-1 .. 0
+            // TD_AV_DIRECT: the lane's alpha block of window wf is loaded two iterations ahead
+            // (acur: this window, anext: the next), the first two before iteration 0
+            const int fk = min(fe >> 3, kW - 1);   // spare lanes: any valid row (they fold nothing)
+            int fks = fk;
+            if constexpr (!kCkAll<ALGO>) ck_row_of<ALGO>(fk, fks);   // the stored row at or before fk
+            const T* ag = ga0 + (size_t)fks * arow + (fe & 7) * 8;
+            T acur[8], anext[8];
+            if constexpr (kAvDirect) {
+                load_block_global<T>(ag + (size_t)(tl - 1) * aws, acur);
+                load_block_global<T>(ag + (size_t)max(tl - 2, 0) * aws, anext);
+            }
             for (int j = 0; j < 3; ++j) {
                 TD_STAMP(b0);
                 const int wf = tl - j + 2;
                 if (lane < nfold && wf <= tl && (fe >> 3) < window_len(gm, wf))
-                    fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
+                    fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm, astore);
                 TD_STAMP(b1);
                 wg_sync_lds();
                 TD_STAMP(b2);
@@ -1754,11 +1837,11 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             fl.Wp = &sm.Wp[0][ke][fl.c][0];
             fl.Bv = &sm.Bv[0][ke][fl.c * 8];
             if constexpr (kCkAll<ALGO>) {
-                fl.Av = &sm.Av[0][ke][fl.c * 8];
+                fl.Av = &sm.Av[0][kAvDirect ? 0 : ke][fl.c * 8];
             } else {
                 int ks;
                 const int r = ck_row_of<ALGO>(ke, ks);
-                fl.Av = &sm.Av[0][r][fl.c * 8];
+                fl.Av = &sm.Av[0][kAvDirect ? 0 : r][fl.c * 8];
                 fl.arot = av_rot<ALGO>(r, fl.c);
                 fl.rec = ke - ks;
                 fl.Gr = &sm.G[0][ks][fl.c][0];
@@ -1771,9 +1854,18 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
+                T afar[8];
+                if constexpr (kAvDirect) load_block_global<T>(ag + (size_t)max(wf - 2, 0) * aws, afar);
 #ifndef TD_DIAG_NOFOLD
-                if (lane < nfold) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
+                if (lane < nfold) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K, acur);
 #endif
+                if constexpr (kAvDirect) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        acur[q] = anext[q];
+                        anext[q] = afar[q];
+                    }
+                }
                 s3 = s3 == 0 ? 2 : s3 - 1;
                 s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
                 s2 ^= 1;
@@ -1790,7 +1882,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             const int wf = tl - j + 2;
 #ifndef TD_DIAG_NOFOLD   // diagnostics only: the B pass without its folds (wrong results)
             if (lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
-                fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
+                fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm, astore);
 #endif
             TD_STAMP(b1);
             wg_sync_lds();
@@ -1985,17 +2077,18 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
 }
 
 // Large batches (more groups than two per CU): three workgroups per CU -- 24 codewords, 12 waves,
-// three per SIMD -- where the build fits them: at most 168 VGPRs without scratch and a third of
-// the CU's LDS.  fp32 Max-Log-MAP fits as it is (143 VGPRs, 42 KB); fp32 log-MAP needs 191 and
-// fp64 240-256 (TD_OCC3_F32LOG builds the fp32 log-MAP one anyway, for the resource report).
+// three per SIMD -- where the build fits them: at most 168 VGPRs without scratch (the build fails
+// on scratch) and a third of the CU's LDS.  fp32 Max-Log-MAP fits as it is (143 VGPRs, 42 KB); the
+// other modes need TD_ROLE_REMAT (fp32 log-MAP 191 -> 78 VGPRs, fp64 240-256 -> 95-106) and fp64
+// also TD_AV_DIRECT (69.9 -> 45.8 KB of LDS).  Measured (B = 12288, one box): fp32 Max-Log-MAP 2370
+// -> 3357 Mbit/s, fp32 log-MAP 1641 -> 2265; fp64 with TD_AV_DIRECT=1 and TD_ROLE_REMAT=2 gained
+// 2-9 % at 12288 and nothing at 32768 (HBM-bound) and lost 9 % at B = 4096, so fp64 stays on two.
 #ifndef TD_OCC3
 #define TD_OCC3 1
 #endif
-#ifndef TD_OCC3_F32LOG
-#define TD_OCC3_F32LOG 0
-#endif
 template <typename T, int ALGO>
-constexpr bool kOcc3 = TD_OCC3 != 0 && kGroupsPerWg == 1 && sizeof(T) == 4 && (ALGO == 1 || TD_OCC3_F32LOG != 0);
+constexpr bool kOcc3 = TD_OCC3 != 0 && kGroupsPerWg == 1 && 3 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
+                       (kRoleRemat<T> || (sizeof(T) == 4 && ALGO == 1));
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kWaves * 64, 3) void turbo_decode_kernel3(DecodeParams<T> p)
 {
@@ -2510,7 +2603,6 @@ constexpr size_t wg_lds()
 }
 static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
 
-static_assert(3 * (sizeof(Smem<float>) + 64) <= 160 * 1024, "three fp32 workgroups per CU");
 
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool probe)
