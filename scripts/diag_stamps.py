@@ -31,13 +31,14 @@ torch.cuda.synchronize()
 c.profile(True)
 bits = c.decode(x)
 _, kms, _ = c.kernel_ms()
-NS = slots // 4
-s = st.cpu().numpy().reshape(G, 4, NS).astype(np.float64)
+NS = 14                 # td_kernels.hip kStampSlots
+NW = slots // NS        # waves per group: 4, or 5 with TD_AREC (R = role 4)
+s = st.cpu().numpy().reshape(G, NW, NS).astype(np.float64)
 L = K + 3
 steps = 2 * iters * L
 print(f"B={B} {prec} {algo} kernel_ms={kms:.3f} errs={int((bits.cpu().numpy() != u).sum())}")
-roles = ["A alpha|fold", "B beta", "F0 loader", "F1 fold"]
-for w in range(4):
+roles = ["A alpha|fold", "B beta", "F0 loader", "F1 fold", "R arec"][:NW]
+for w in range(NW):
     fw, fwait, bw, bwait = (s[:, w, i].mean() / steps for i in range(4))
     print(f"  {roles[w]:14s} per SISO-step: F work {fw:7.1f}  F wait {fwait:7.1f}  B work {bw:7.1f}  B wait {bwait:7.1f}"
           f"  (slot4 {s[:, w, 4].mean() / steps:6.1f})")
@@ -46,21 +47,23 @@ clk = kc.sum() / kr.sum() * 0.1   # GHz (realtime ticks at 100 MHz)
 acc = s[:, :, 0:4].sum(axis=2)
 print(f"  clock {clk:.3f} GHz; kernel {kc.mean() / steps:.1f} cycles per SISO-step, of which the pass stamps cover "
       f"{acc.mean() / steps:.1f} (unstamped: SISO prologues / epilogues, {(kc.mean() - acc.mean()) / steps:.1f})")
-for w in range(4):
+for w in range(NW):
     print(f"  {roles[w]:14s} per SISO-step: SISO calls {s[:, w, 9].mean() / steps:7.1f}  SISO-end barrier "
           f"{s[:, w, 10].mean() / steps:6.1f}  in-SISO unstamped {(s[:, w, 9] - s[:, w, 0:4].sum(axis=1)).mean() / steps:6.1f}"
           + (f"  F prologue {s[:, w, 11].mean() / steps:6.1f}" if NS > 11 else "")
           + (f"  B prologue {s[:, w, 12].mean() / steps:6.1f}  first tile {s[:, w, 13].mean() / steps:6.1f}" if NS > 13 and w == 2 else ""))
-hw = st.cpu().numpy().reshape(G, 4, NS)[:, :, 6].astype(np.int64)
+hw = st.cpu().numpy().reshape(G, NW, NS)[:, :, 6].astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15
 se = (hw >> 13) & 7
 distinct = np.array([len(set(simd[g])) for g in range(G)])
 print("  waves of a group on distinct SIMDs: " + ", ".join(f"{k}:{int((distinct == k).sum())}" for k in (1, 2, 3, 4)))
+if NW == 5:
+    print(f"  R shares its SIMD with A in {int((simd[:, 4] == simd[:, 0]).sum())} groups, B {int((simd[:, 4] == simd[:, 1]).sum())}, F0 {int((simd[:, 4] == simd[:, 2]).sum())}, F1 {int((simd[:, 4] == simd[:, 3]).sum())}")
 same = lambda a, b: int((simd[:, a] == simd[:, b]).sum())
 print(f"  A/B share SIMD in {same(0, 1)} groups, A/F0 {same(0, 2)}, A/F1 {same(0, 3)}, B/F0 {same(1, 2)}, B/F1 {same(1, 3)}")
 # workgroups resident on the same CU (XCC, SE, SH, CU): which roles of the two share a SIMD
-xcc = st.cpu().numpy().reshape(G, 4, NS)[:, 0, 5].astype(np.int64) & 0xF
+xcc = st.cpu().numpy().reshape(G, NW, NS)[:, 0, 5].astype(np.int64) & 0xF
 sh = (hw >> 12) & 1
 key = [(int(xcc[g]), int(se[g, 0]), int(sh[g, 0]), int(cu[g, 0])) for g in range(G)]
 from collections import Counter, defaultdict  # noqa: E402
@@ -73,8 +76,8 @@ for v in by.values():
     for i in range(len(v)):
         for j in range(i + 1, len(v)):
             a, b = v[i], v[j]
-            for ra in range(4):
-                for rb in range(4):
+            for ra in range(NW):
+                for rb in range(NW):
                     if simd[a, ra] == simd[b, rb]:
                         pairs[(roles[ra].split()[0], roles[rb].split()[0])] += 1
     if len(v) == 2 and len(pairs) < 0:

@@ -976,7 +976,7 @@ int td_debug_placement_rule(const float* ms, int n)
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
-    return 4 * 14;   // [wave][slot] (td_kernels.hip kStampSlots)
+    return td::kGroupWaves * 14;   // [wave][slot] (td_kernels.hip kStampSlots)
 #else
     return 0;
 #endif

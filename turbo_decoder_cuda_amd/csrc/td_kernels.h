@@ -30,6 +30,11 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
 constexpr int kPermPad = 16;         // spare ints after pi / pinv: the loader stages window-sized chunks
+// TD_AREC: alpha recomputed in the B pass by a fifth wave per codeword group (td_kernels.hip)
+#ifndef TD_AREC
+#define TD_AREC 0
+#endif
+constexpr int kGroupWaves = TD_AREC ? 5 : 4;   // waves per codeword group (stamp slots per group)
 constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
 // alpha scratch (astore) of one codeword group: L rows of 64 (8 codewords x 8 states) plus a pad of
 // TD_APAD elements between the groups' streams (a knob: pads of 512 B, 4 KiB and 32.5 KiB left the

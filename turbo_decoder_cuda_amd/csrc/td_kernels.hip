@@ -280,7 +280,12 @@ __device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneC
 //                         codeword) item per lane, both input bits in the same lane.
 // Only the two recursions are serial chains; nothing else waits on them but the barriers.  The
 // barriers are raw `s_waitcnt lgkmcnt(0); s_barrier`, so prefetched global loads stay in flight.
-constexpr int kWaves = 4;                            // waves per codeword group
+// TD_AREC (td_kernels.h): the F pass streams only one alpha row per window (alpha_raw entering the
+// window's first step, the checkpoint) and a fifth wave R recomputes alpha over each window in the B
+// pass, beside beta, into an LDS ring the folds read -- the alpha scratch stream (63 % of the HBM
+// traffic) shrinks twelvefold, and the Av ring to two windows, so that three workgroups fit a CU.
+constexpr bool kArec = TD_AREC != 0;
+constexpr int kWaves = kGroupWaves;                  // waves per codeword group (5 with TD_AREC)
 #ifndef TD_GROUPS_PER_WG
 #define TD_GROUPS_PER_WG 1
 #endif
@@ -304,7 +309,8 @@ constexpr int kFoldA = ALGO == 0 ? TD_FOLD_A : kFoldPerWave;
 #define TD_ML_FOLD_MAP 1   // Max-Log-MAP fold items split by recompute depth (siso_wg B pass)
 #endif
 static_assert(TD_FOLD_A <= kLanes && kTile - TD_FOLD_A <= kLanes, "one fold item per lane");
-constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
+constexpr int kAvSlots = kArec ? 2 : 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3);
+                                          // TD_AREC: written by R one iteration before its fold
 // TD_AV_DIRECT: the fold lanes load their alpha blocks (8 states, 64 B in fp64) from the HBM scratch
 // into registers one window ahead, instead of the loader copying whole windows into an LDS ring
 // (Av): the ring is 24.6 KB of the fp64 workgroup's 69.9 KB of LDS, without it three workgroups fit
@@ -313,6 +319,10 @@ constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold
 #define TD_AV_DIRECT 0
 #endif
 constexpr bool kAvDirect = TD_AV_DIRECT != 0;
+static_assert(!(kAvDirect && kArec), "TD_AV_DIRECT and TD_AREC exclude each other");
+// every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
+template <int ALGO>
+constexpr bool kFoldRows = kArec || kCkAll<ALGO>;
 
 // Loader staging.  Window inputs travel HBM -> LDS by DMA (global_load_lds_dwordx4: no VGPR
 // destination, completion counted by vmcnt; LDS target = wave-uniform base + 16 * lane) and the
@@ -326,18 +336,24 @@ template <typename T>
 constexpr int kTileChunks = 3 * kStreamChunks<T> + 2 * (kW / 4);
 template <typename T>
 constexpr int kTileDma = (kTileChunks<T> + kLanes - 1) / kLanes;   // DMA instructions per staged window
+// Staging slots hold exactly a window's chunks: the last DMA of a window (and the tempmax DMA) run on
+// the lanes that have a chunk only, so the slots carry no spare lanes' landing space.
+template <typename T>
+constexpr int kStageBytes = kTileChunks<T> * 16;
+template <typename T>
+constexpr int kTmStageBytes = kStreamChunks<T> * 16;
 
 template <typename T>
 struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
-    int Wp[3][kW][kCw][2];     // extrinsic / decision write positions (pi or pinv, pi), same ring
+    int Wp[3][kW][2];          // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
     T Av[kAvDirect ? 1 : kAvSlots][kAvDirect ? 1 : kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state
                                                                     // (fold input, DMA from HBM; unused: TD_AV_DIRECT)
     T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
-    alignas(16) unsigned char stage[3][kTileDma<T> * kDmaBytes];   // loader: staged window inputs
-    alignas(16) unsigned char tmstage[3][kDmaBytes];                // loader: staged tempmax of a window
+    alignas(16) unsigned char stage[3][kStageBytes<T>];     // loader: staged window inputs
+    alignas(16) unsigned char tmstage[3][kTmStageBytes<T>];  // loader: staged tempmax of a window
 };
 
 // Fold-input rows (Av, Bv): a (row, codeword) block holds the 8 states, 64 B in fp64 (4 chunks of
@@ -564,7 +580,8 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const int r = min(max(ch - 3 * nc, 0), 2 * (kW / 4) - 1);
         const int* pb = r < kW / 4 ? pperm : gm.pi;
         const char* pw = reinterpret_cast<const char*>(pb + tc * kW + (r % (kW / 4)) * 4);
-        dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);   // spare lanes repeat the last chunk
+        if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
+            dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
     }
 }
 
@@ -575,7 +592,8 @@ __device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, 
     constexpr int E = 16 / (int)sizeof(T);
     const int e0 = min(lane, kStreamChunks<T> - 1) * E;
     const int i = min(max(t * kW + (e0 >> 3), 0), gm.L - 1);
-    dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
+    if (lane < kStreamChunks<T>)   // the lanes with a chunk only (kTmStageBytes)
+        dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
 }
 
 // staged tempmax of window t -> its LDS slot (beta input)
@@ -601,7 +619,7 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
     const T* sl = sy + 2 * kTile;
     const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile);   // [kW] pi-or-pinv, then [kW] pi
     T* g = &sm.G[t % 3][0][0][0];
-    int* w = &sm.Wp[t % 3][0][0][0];
+    int* w = &sm.Wp[t % 3][0][0];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int e = lane + kLanes * q;
@@ -614,8 +632,10 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
             g[4 * e + 1] = (ys - yp) + hla;
             g[4 * e + 2] = ys;
             g[4 * e + 3] = la;
-            w[2 * e] = sw[k];
-            w[2 * e + 1] = sw[kW + k];
+            if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
+                w[2 * k] = sw[k];
+                w[2 * k + 1] = sw[kW + k];
+            }
         }
     }
 }
@@ -663,7 +683,7 @@ __device__ __forceinline__ int ck_row_of(int k, int& ks)
 template <typename T, int ALGO>
 constexpr int alpha_dma_count()
 {
-    return kAvDirect ? 0 : kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
+    return (kAvDirect || kArec) ? 0 : kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
 }
 static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
@@ -770,7 +790,7 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
 #ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
     if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
 #else
-    if ((kCkPh<ALGO> >> PH) & 1) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
+    if (!kArec && ((kCkPh<ALGO> >> PH) & 1)) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
 #endif
     gstore(ptm, m);
     return h;
@@ -902,7 +922,7 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr ((kCkPh<0> >> PH) & 1) gstore(ga + K * arow + lc.st_off[PH], alpha);   // log-MAP only
+        if constexpr (!kArec && ((kCkPh<0> >> PH) & 1)) gstore(ga + K * arow + lc.st_off[PH], alpha);   // log-MAP only
         gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
@@ -1000,7 +1020,7 @@ struct AlphaSchedS {
 #ifdef TD_DIAG_SPARSE_ASCHED   // diagnostics only (wrong log-MAP results): alpha stored at phase 0 only
             if constexpr (PH == 0)
 #endif
-            if constexpr ((kCkPh<ALGO> >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
+            if constexpr (!kArec && ((kCkPh<ALGO> >> PH) & 1)) astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
@@ -1009,7 +1029,7 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr ((kCkPh<ALGO> >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha, arow);
+            if constexpr (!kArec && ((kCkPh<ALGO> >> PH) & 1)) astore_row<T, K>(sa, va[PH], alpha, arow);
             tm_keep<T, K>(tbh, m, stm, vtm);
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
@@ -1079,6 +1099,7 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
 {
     (void)chain_st;
     const int tb = t % 3;
+    if constexpr (kArec) gstore(ga + lc.st_off[0], a);   // checkpoint: alpha_raw entering the window (row 0)
 #if TD_SCHED
     if constexpr (ALGO == 0) {
         if (n == kW) {
@@ -1138,6 +1159,101 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
         a = alpha_step<T, ALGO, 1>(a, i1, lut, lc, pa1 + k * arow, ptm);
     }
     return a;
+}
+
+// ------------------------------------------------------------------ alpha recompute (TD_AREC)
+#ifndef TD_AREC_PRIO
+#define TD_AREC_PRIO 2   // VALU priority of wave R in the B pass (beta's is TD_BETA_PRIO_*)
+#endif
+#ifndef TD_AREC_ROLES
+#define TD_AREC_ROLES 1   // wg_pos: R on wave 2, the loader on wave 4
+#endif
+// Wave R, B pass: alpha over window t again, from the F pass's checkpoint (alpha_raw entering the
+// window's first step, stored by wave A at row 0 of the window's scratch), with wave A's arithmetic
+// step for step (alpha_tempmax, the two fma, the table max*: bit-identical), publishing alpha[.][i]
+// of every step by state into the Av ring (rotated blocks, as beta publishes Bv) instead of HBM.
+template <typename T, int ALGO, int PH>
+__device__ __forceinline__ T arec_step(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc, T* Avw, int k)
+{
+    T an;
+    const T m = alpha_tempmax<T, PH>(a, an);
+    const T alpha = a - m, ap = an - m;
+    const T xs = fma(lc.a_sg[PH], in.gs, alpha);
+    const T xp = fma(lc.a_pg[PH], in.gp, ap);
+    if constexpr (ALGO == 0) {
+        const T d = xp - xs;
+        const LutRow r = lut_row(d);
+        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        Avw[k * kLanes + rot_off<T>(lc.st_off[PH], k)] = alpha;   // behind the table read
+        return sched_finish(xs, xp, d, thr, lo, hi);
+    } else {
+        Avw[k * kLanes + rot_off<T>(lc.st_off[PH], k)] = alpha;
+        return vmax(xs, xp);
+    }
+}
+
+// a full window, scheduled like AlphaSchedS: [chain to the row address] [row reads] [operand reads
+// of step K+2] [the Av write] [select + add]
+template <typename T, int ALGO, int K>
+struct AlphaSchedR {
+    static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
+                                               int c, const LaneConst<T>& lc, T* Avw)
+    {
+        constexpr int PH = K % 3;
+        const StepIn<T> in = op[K % 3];
+        T an;
+        const T m = alpha_tempmax<T, PH>(a, an);
+        const T alpha = a - m, ap = an - m;
+        const T xs = fma(lc.a_sg[PH], in.gs, alpha);
+        const T xp = fma(lc.a_pg[PH], in.gp, ap);
+        if constexpr (ALGO == 0) {
+            const T d = xp - xs;
+            const LutRow r = lut_row(d);
+            __builtin_amdgcn_sched_barrier(0);
+            const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            Avw[K * kLanes + rot_off<T>(lc.st_off[PH], K)] = alpha;
+            __builtin_amdgcn_sched_barrier(0);
+            a = sched_finish(xs, xp, d, thr, lo, hi);
+        } else {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            Avw[K * kLanes + rot_off<T>(lc.st_off[PH], K)] = alpha;
+            __builtin_amdgcn_sched_barrier(0);
+            a = vmax(xs, xp);
+        }
+        AlphaSchedR<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, Avw);
+    }
+};
+template <typename T, int ALGO>
+struct AlphaSchedR<T, ALGO, kW> {
+    static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
+                                               const LaneConst<T>&, T*)
+    {
+    }
+};
+
+// alpha of the n steps of window t (G ring slot tb) from its checkpoint a, into Avw = Av[t & 1]
+template <typename T, int ALGO>
+__device__ __forceinline__ void arec_window(T a, int tb, int n, const Smem<T>& sm, const T* lut, int c,
+                                            const LaneConst<T>& lc, T* Avw)
+{
+    if (n == kW) {
+        StepIn<T> op[3];
+        op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
+        op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
+        __builtin_amdgcn_sched_barrier(0);
+        AlphaSchedR<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, Avw);
+        return;
+    }
+    for (int k = 0; k < n; k += 3) {   // the last window (window starts are = 0 mod 3)
+        a = arec_step<T, ALGO, 0>(a, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, Avw, k);
+        if (k + 1 < n) a = arec_step<T, ALGO, 1>(a, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc, Avw, k + 1);
+        if (k + 2 < n) a = arec_step<T, ALGO, 2>(a, alpha_in<T, 2>(sm, tb, k + 2, c, lc), lut, lc, Avw, k + 2);
+    }
 }
 
 #ifndef TD_BETA_BATCH
@@ -1317,11 +1433,11 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     const int i = t * kW + k;
     const T* g = &sm.G[t % 3][k][c][0];
     const T P = g[0], Q = g[1], ys = g[2], la = g[3];
-    const int wperm = sm.Wp[t % 3][k][c][0], wbit = sm.Wp[t % 3][k][c][1];
+    const int wperm = sm.Wp[t % 3][k][0], wbit = sm.Wp[t % 3][k][1];
     T a[8], b[8], t0[8], t1[8];
     const T* bv = &sm.Bv[t & 1][k][c * 8];
     load_block<T>(bv, k, b);
-    if constexpr (!kCkAll<ALGO>) {
+    if constexpr (!kFoldRows<ALGO>) {
         // alpha[.][i] from the last stored step ks <= k, recomputed through the steps in between
         // exactly as the alpha wave computed them (:975-1001)
         int ks;
@@ -1389,7 +1505,7 @@ template <typename T>
 struct FoldLane {
     int k, c;
     const T* G;      // &sm.G[0][k][c][0]
-    const int* Wp;   // &sm.Wp[0][k][c][0]
+    const int* Wp;   // &sm.Wp[0][k][0]
     const T* Bv;     // &sm.Bv[0][k][c * 8]
     const T* Av;     // &sm.Av[0][r][c * 8], r = the stored row of step k (or the one before it)
     int arot;        // the block rotation of that row (av_rot)
@@ -1405,7 +1521,7 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const int k = fl.k;
     const T* g = fl.G + s3 * (kW * kCw * 4);
     const T P = g[0], Q = g[1], ys = g[2], la = g[3];
-    const int* wp = fl.Wp + s3 * (kW * kCw * 2);
+    const int* wp = fl.Wp + s3 * (kW * 2);
     const int wperm = wp[0], wbit = wp[1];
     T a[8], b[8], t0[8], t1[8];
     load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
@@ -1413,9 +1529,9 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = ain[j];   // loaded one window ahead (siso_wg)
     } else {
-        load_block<T>(fl.Av + s4 * (kW * kLanes), kCkAll<ALGO> ? k : fl.arot, a);
+        load_block<T>(fl.Av + s4 * (kW * kLanes), kFoldRows<ALGO> ? k : fl.arot, a);
     }
-    if constexpr (!kCkAll<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
+    if constexpr (!kFoldRows<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
         const T* gr = fl.Gr + s3 * (kW * kCw * 4);
         for (int q = 0; q < fl.rec; ++q) alpha_recompute<T, ALGO>(a, gr[q * kCw * 4], gr[q * kCw * 4 + 1], lut);
     }
@@ -1559,6 +1675,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
                     if (TD_AOP_FIRST) __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
+                    if constexpr (kArec) astore_row<T, 0>(sa, va[0], a, arow);   // checkpoint (row 0)
                     TD_CHAIN_T0(c0);
                     AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh, arow);
                     TD_CHAIN_ACC(c0);
@@ -1683,10 +1800,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
-    } else if (dst.sys2_out) {
+    } else if (dst.sys2_out && wave != 4) {
         // waves 1 and 3, first SISO: SISO2's systematic input sys2[g][i][c] = sys1[g][pi(i)][c]
         // (i < K; :1109-1113), one element of window t per lane (96 of 128 lanes) with pi(i) from
-        // the ring slot of window t (Wp[.][k][c][1], staged by the loader), loaded in iteration t
+        // the ring slot of window t (Wp[.][k][1], staged by the loader), loaded in iteration t
         // and stored in t+1, so no wave ever waits on HBM before a barrier.  This is
         // demux_perm_kernel's work, done by the waves the F pass leaves idle.
         wg_sync_lds();
@@ -1701,7 +1818,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         int ip = -1;   // row of the pending store
         for (int t = 0; t < nT; ++t) {
             TD_STAMP(f0);
-            const int pi_i = min(max(sm.Wp[t % 3][k][c][1], 0), gm.K - 1);   // spare rows past K: any valid row
+            const int pi_i = min(max(sm.Wp[t % 3][k][1], 0), gm.K - 1);   // spare rows past K: any valid row
             const T nv = s1[(size_t)pi_i * kCw];
             if (ip >= 0) s2[(size_t)ip * kCw] = v;
             const int i = t * kW + k;
@@ -1733,8 +1850,32 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     }
 
-    // ===================================== B pass (waves 0, 1, 3)
-    if (wave == 1) {
+    // ===================================== B pass (waves 0, 1, 3; 4 with TD_AREC)
+    if (kArec && wave == 4) {
+        // R: alpha over window wb = tl - j + 1 (beta's window) into Av[wb & 1], folded next
+        // iteration; the checkpoint of the next window is loaded one iteration ahead
+        const int c = lane >> 3;
+        LaneConst<T> lc;
+        lane_setup(lt, lane, lc);
+        const T* lut = lut_col(sm, lane);
+        const int cko = lc.st_off[0];
+        T ck = ga0[(size_t)tl * aws + cko];
+        __builtin_amdgcn_s_setprio(TD_AREC_PRIO);
+        for (int j = 0; j < nB; ++j) {
+            TD_STAMP(b0);
+            const int wb = tl - j + 1;
+            if (wb >= 0 && wb <= tl) {
+                const T cn = ga0[(size_t)max(wb - 1, 0) * aws + cko];
+                arec_window<T, ALGO>(ck, wb % 3, window_len(gm, wb), sm, lut, c, lc, &sm.Av[wb & 1][0][0]);
+                ck = cn;
+            }
+            TD_STAMP(b1);
+            wg_sync_lds();
+            TD_STAMP(b2);
+            TD_ACC(2, b0, b1);
+            TD_ACC(3, b1, b2);
+        }
+    } else if (wave == 1) {
         // beta over window wb = tl - j + 1 (its tempmax was staged last iteration)
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
@@ -1792,7 +1933,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
         int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
-        if constexpr (!kCkAll<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP)) {
+        if constexpr (!kFoldRows<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP)) {
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
             // takes the 32 items of the phase furthest from a kept row (pd), the fold wave beside
             // the other workgroup's beta (F1) the 64 items of the other two phases.  Max-Log-MAP
@@ -1804,14 +1945,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
         }
         int j0 = 0;
-        if (TD_FOLD_FAST && (ALGO == 0 || kAvDirect) && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
+        if (TD_FOLD_FAST && (ALGO == 0 || kAvDirect || kArec) && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
             // here iterations 3 .. nB-1, i.e. the full windows wf = tl-1 .. 0
             // TD_AV_DIRECT: the lane's alpha block of window wf is loaded two iterations ahead
             // (acur: this window, anext: the next), the first two before iteration 0
             const int fk = min(fe >> 3, kW - 1);   // spare lanes: any valid row (they fold nothing)
             int fks = fk;
-            if constexpr (!kCkAll<ALGO>) ck_row_of<ALGO>(fk, fks);   // the stored row at or before fk
+            if constexpr (!kFoldRows<ALGO>) ck_row_of<ALGO>(fk, fks);   // the stored row at or before fk
             const T* ag = ga0 + (size_t)fks * arow + (fe & 7) * 8;
             T acur[8], anext[8];
             if constexpr (kAvDirect) {
@@ -1834,9 +1975,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             fl.c = fe & 7;
             const int ke = min(fl.k, kW - 1);   // spare lanes: any valid row (they fold nothing)
             fl.G = &sm.G[0][ke][fl.c][0];
-            fl.Wp = &sm.Wp[0][ke][fl.c][0];
+            fl.Wp = &sm.Wp[0][ke][0];
             fl.Bv = &sm.Bv[0][ke][fl.c * 8];
-            if constexpr (kCkAll<ALGO>) {
+            if constexpr (kFoldRows<ALGO>) {
                 fl.Av = &sm.Av[0][kAvDirect ? 0 : ke][fl.c * 8];
             } else {
                 int ks;
@@ -1940,7 +2081,7 @@ struct WgPos {
     int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
     int lane;
     int g;       // global codeword group index
-    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (2: none)
+    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (3: none)
     int slot;
 };
 
@@ -1974,6 +2115,10 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
     const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
     const int lane = (int)(threadIdx.x & 63);
     const int g = (int)blockIdx.x * kGroupsPerWg + h;
+    // TD_AREC: waves 0, 1, 2, 3, 4 -> A, B, R, F1, F0 (roles 0, 1, 4, 3, 2): with waves w and w+4 on
+    // one SIMD the two B-pass chains (B, R) each have a SIMD of their own within the workgroup,
+    // and A shares its SIMD with the loader (as TD_ROLE_MAP 2 pairs them)
+    if (kWaves == 5) return WgPos{h, TD_AREC_ROLES ? (wave == 2 ? 4 : (wave == 4 ? 2 : wave)) : wave, lane, g, 0, 3};
     if (TD_ROLE_MAP == 2 && kGroupsPerWg == 1 && role_cus > 0 && slots) {
         __shared__ int s_simd[kWaves];
         __shared__ int s_slot;
@@ -2008,7 +2153,7 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
     } else {
         role = ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + (second ? 3 : 0) & 3;
     }
-    return WgPos{h, role, lane, g, 0, 2};
+    return WgPos{h, role, lane, g, 0, 3};   // slot 3: none (wg_release)
 }
 
 // end of the kernel: give the CU slot back (all waves of the workgroup are past their work)
@@ -2071,7 +2216,7 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
 }
 
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
 {
     turbo_decode_body<T, ALGO>(p);
 }
@@ -2090,7 +2235,7 @@ template <typename T, int ALGO>
 constexpr bool kOcc3 = TD_OCC3 != 0 && kGroupsPerWg == 1 && 3 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
                        (kRoleRemat<T> || (sizeof(T) == 4 && ALGO == 1));
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kWaves * 64, 3) void turbo_decode_kernel3(DecodeParams<T> p)
+__global__ __launch_bounds__(kWaves * 64, kArec ? 4 : 3) void turbo_decode_kernel3(DecodeParams<T> p)
 {
     if constexpr (kOcc3<T, ALGO>) turbo_decode_body<T, ALGO>(p);
 }
@@ -2099,7 +2244,7 @@ __global__ __launch_bounds__(kWaves * 64, 3) void turbo_decode_kernel3(DecodePar
 // turbo_decode_kernel under its own symbol, so that kernel traces and PMC passes of a decode list
 // the one-iteration probe launches apart from the decode's own launches.
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void turbo_placement_probe_kernel(
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void turbo_placement_probe_kernel(
     DecodeParams<T> p)
 {
     turbo_decode_body<T, ALGO>(p);
@@ -2107,7 +2252,7 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void 
 
 // Standalone SISO (Log_MAP_decoder) over interleaved [G][L][8] inputs.
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
+__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
                                                                                           int terminated)
 {
     const WgPos w = wg_pos(p.role_cus, p.cu_slots);
