@@ -94,17 +94,18 @@ def _decode_bits(K, f1, f2, iters, flow, algo="logmap", precision="f64"):
     return bits.cpu().numpy()
 
 
-@pytest.mark.parametrize("precision,algo,K,f1,f2", [("f32", "maxlog", 40, 3, 10), ("f32", "logmap", 40, 3, 10),
-                                                    ("f64", "maxlog", 40, 3, 10), ("f64", "logmap", 40, 3, 10),
-                                                    ("f64", "logmap", 1024, 31, 64)])
-def test_three_workgroups_per_cu(monkeypatch, precision, algo, K, f1, f2):
-    """B = 6150 is 769 codeword groups, more than two per CU, so the decode runs
-    turbo_decode_kernel3 (three workgroups per CU) where the build has it.  Its bits and Le equal
-    the two-workgroup kernel's (TD_OCC3=0) exactly -- with an Le dump (the generic fold) and
-    without (the fast fold) -- and a sample of codewords matches the oracle: fp64 bit for bit
-    (Le to 1e-9); fp32 as test_maxlog_vs_oracle / test_f32_logmap_vs_oracle_f32 (log-MAP: the
-    last iteration's bits on converged frames at 1.0 dB)."""
-    B, iters = 6150, 3
+@pytest.mark.parametrize("precision,algo,K,f1,f2,B", [("f32", "maxlog", 40, 3, 10, 5000), ("f32", "logmap", 40, 3, 10, 5000),
+                                                      ("f32", "maxlog", 40, 3, 10, 6150), ("f32", "logmap", 40, 3, 10, 6150),
+                                                      ("f64", "maxlog", 40, 3, 10, 6150), ("f64", "logmap", 40, 3, 10, 6150),
+                                                      ("f64", "logmap", 1024, 31, 64, 6150)])
+def test_three_workgroups_per_cu(monkeypatch, precision, algo, K, f1, f2, B):
+    """More codeword groups than two per CU (B = 5000: 625 groups; 6150: 769, more than three per
+    CU on 256 CUs) run turbo_decode_kernel3 / turbo_decode_kernel4 (three / four workgroups per CU)
+    where the build has them (fp32).  Bits and Le equal the two-workgroup kernel's (TD_OCC3=0)
+    exactly -- with an Le dump (the generic fold) and without (the fast fold) -- and a sample of
+    codewords matches the oracle: fp64 bit for bit (Le to 1e-9); fp32 as test_maxlog_vs_oracle /
+    test_f32_logmap_vs_oracle_f32 (log-MAP: the last iteration's bits on converged frames at 1.0 dB)."""
+    iters = 3
     _, flow = O.synth_batch(K, f1, f2, 0.3 if (algo == "maxlog" or precision == "f64") else 1.0, 31, B)
     if precision == "f32":
         flow = flow.astype(np.float32)

@@ -2081,7 +2081,7 @@ struct WgPos {
     int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
     int lane;
     int g;       // global codeword group index
-    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (3: none)
+    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (4: none)
     int slot;
 };
 
@@ -2118,7 +2118,7 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
     // TD_AREC: waves 0, 1, 2, 3, 4 -> A, B, R, F1, F0 (roles 0, 1, 4, 3, 2): with waves w and w+4 on
     // one SIMD the two B-pass chains (B, R) each have a SIMD of their own within the workgroup,
     // and A shares its SIMD with the loader (as TD_ROLE_MAP 2 pairs them)
-    if (kWaves == 5) return WgPos{h, TD_AREC_ROLES ? (wave == 2 ? 4 : (wave == 4 ? 2 : wave)) : wave, lane, g, 0, 3};
+    if (kWaves == 5) return WgPos{h, TD_AREC_ROLES ? (wave == 2 ? 4 : (wave == 4 ? 2 : wave)) : wave, lane, g, 0, 4};
     if (TD_ROLE_MAP == 2 && kGroupsPerWg == 1 && role_cus > 0 && slots) {
         __shared__ int s_simd[kWaves];
         __shared__ int s_slot;
@@ -2127,8 +2127,8 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
         const int simd = (int)((hw >> 4) & 3);
         const int key = (int)((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
         if (threadIdx.x == 0) {
-            int slot = 0;   // the first free of slots 0..2 (3: none)
-            while (slot < 3 && (atomicOr(&slots[key], 1u << slot) & (1u << slot))) ++slot;
+            int slot = 0;   // the first free of slots 0..3 (4: none)
+            while (slot < 4 && (atomicOr(&slots[key], 1u << slot) & (1u << slot))) ++slot;
             s_slot = slot;
         }
         if (lane == 0) s_simd[wave] = simd;
@@ -2140,9 +2140,10 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
             for (int b = a + 1; b < kWaves; ++b) distinct = distinct && s_simd[a] != s_simd[b];
         const int slot = s_slot;
         const int base = distinct ? simd : wave;
-        // slot 2 (turbo_decode_kernel3's third workgroup): role = SIMD ^ 1, so that the three
-        // workgroups' alpha chains (and their beta chains) sit on three different SIMDs
-        return WgPos{h, slot == 1 ? base ^ TD_SLOT_XOR : (slot == 2 ? base ^ 1 : base), lane, g, key, slot};
+        // slots 2, 3 (turbo_decode_kernel3 / 4): role = SIMD ^ 1, SIMD ^ 3, so that the workgroups'
+        // alpha chains (and their beta chains) sit on different SIMDs
+        const int rx = slot == 1 ? TD_SLOT_XOR : (slot == 2 ? 1 : (slot == 3 ? 3 : 0));
+        return WgPos{h, base ^ rx, lane, g, key, slot};
     }
     const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
     int role;
@@ -2153,13 +2154,13 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
     } else {
         role = ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + (second ? 3 : 0) & 3;
     }
-    return WgPos{h, role, lane, g, 0, 3};   // slot 3: none (wg_release)
+    return WgPos{h, role, lane, g, 0, 4};   // slot 4: none (wg_release)
 }
 
 // end of the kernel: give the CU slot back (all waves of the workgroup are past their work)
 __device__ __forceinline__ void wg_release(const WgPos& w, unsigned* slots)
 {
-    if (w.slot < 3) {
+    if (w.slot < 4) {
         __syncthreads();
         if (threadIdx.x == 0) atomicAnd(&slots[w.slot_key], ~(1u << w.slot));
     }
@@ -2238,6 +2239,20 @@ template <typename T, int ALGO>
 __global__ __launch_bounds__(kWaves * 64, kArec ? 4 : 3) void turbo_decode_kernel3(DecodeParams<T> p)
 {
     if constexpr (kOcc3<T, ALGO>) turbo_decode_body<T, ALGO>(p);
+}
+
+// More than three groups per CU: four workgroups per CU (16 waves, at most 128 VGPRs, a quarter of
+// the LDS) where they fit: fp32 (36.7 KB of LDS, 67-79 VGPRs with TD_ROLE_REMAT).
+#ifndef TD_OCC4
+#define TD_OCC4 1
+#endif
+template <typename T, int ALGO>
+constexpr bool kOcc4 = TD_OCC4 != 0 && !kArec && kGroupsPerWg == 1 && 4 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
+                       kRoleRemat<T>;
+template <typename T, int ALGO>
+__global__ __launch_bounds__(kWaves * 64, 4) void turbo_decode_kernel4(DecodeParams<T> p)
+{
+    if constexpr (kOcc4<T, ALGO>) turbo_decode_body<T, ALGO>(p);
 }
 
 // td_reserve's workspace-placement probe (td_api.cpp place_ws): the same code as
@@ -2749,13 +2764,50 @@ constexpr size_t wg_lds()
 static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
 
 
+// turbo_decode_kernel3's LDS: never less than a quarter of the CU's plus 1 KB, so that at most three
+// of its workgroups share a CU (the fp32 Smem alone would let four in)
+template <typename T>
+constexpr size_t wg_lds3()
+{
+    return sizeof(Smem<T>) > 160 * 1024 / 4 + 1024 ? sizeof(Smem<T>) : 160 * 1024 / 4 + 1024;
+}
+
+// Workgroups per CU for a decode of p.G groups: the fewest expected kernel time over the occupancies
+// the build has (2; 3 and 4 where kOcc3 / kOcc4), counting whole dispatch rounds of N groups per CU
+// at the measured time of a round with N per CU (fp32, relative to N = 2; one box, K = 6144: log-MAP
+// 1.17 for 3, 1.39 for 4; Max-Log-MAP 1.07, 1.29) and the last partial round at the time of its own
+// groups per CU.
+template <typename T, int ALGO>
+int occupancy_pick(const DecodeParams<T>& p)
+{
+    if (!p.occ3 || p.role_cus <= 0 || p.G <= 2 * p.role_cus) return 2;
+    const double t_rel[5] = {1.0, 1.0, 1.0, ALGO == 1 ? 1.07 : 1.17, ALGO == 1 ? 1.29 : 1.39};
+    auto est = [&](int n) {
+        const long per_round = (long)n * p.role_cus;
+        const long full = p.G / per_round, rem = p.G % per_round;
+        const int last = (int)((rem + p.role_cus - 1) / p.role_cus);
+        return full * t_rel[n] + (rem ? t_rel[last] : 0.0);
+    };
+    int best = 2;
+    if (kOcc3<T, ALGO> && est(3) < est(best)) best = 3;
+    if (kOcc4<T, ALGO> && est(4) < est(best)) best = 4;
+    return best;
+}
+
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool probe)
 {
-    if (kOcc3<T, ALGO> && !probe && p.occ3 && p.role_cus > 0 && p.G > 2 * p.role_cus) {
-        hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel3<T, ALGO>), sizeof(Smem<T>));
+    const int occ = probe ? 2 : occupancy_pick<T, ALGO>(p);
+    if (occ == 4) {
+        hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel4<T, ALGO>), sizeof(Smem<T>));
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((turbo_decode_kernel3<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
+        hipLaunchKernelGGL((turbo_decode_kernel4<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
+        return hipGetLastError();
+    }
+    if (occ == 3) {
+        hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel3<T, ALGO>), wg_lds3<T>());
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((turbo_decode_kernel3<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), wg_lds3<T>(), st, p);
         return hipGetLastError();
     }
     const void* k = probe ? reinterpret_cast<const void*>(&turbo_placement_probe_kernel<T, ALGO>)
