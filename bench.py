@@ -474,21 +474,24 @@ def pcie_inclusive(a, codec, llr, dev, stream):
 
 
 def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
-    """Other arithmetic modes on the same batch (configs 3, fp32), and BASELINE config 5 (sliding
-    window 64 with overlap 30) at its own batch of 32768 codewords: frames 0..32767 of the same
-    srand(SEED) stream, made on the device by the bench's codec."""
+    """Other arithmetic modes on the same batch (configs 3, fp32), BASELINE config 5 (sliding
+    window 64 with overlap 30) at its own batch of 32768 codewords, and the exact schedule at config
+    4's per-GPU shard (32768; fp32 there runs three or four workgroups per CU): frames
+    0..32767 of the same srand(SEED) stream, made on the device by the bench's codec."""
     import torch
 
     from turbo_decoder_cuda_amd import TurboCodec
 
     res = {}
-    cases = [(p, g, 0) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog"))]
-    cases += [(p, g, 64) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
+    cases = [(p, g, 0, False) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog"))]
+    cases += [(p, g, 64, True) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
+    if a.batch != CONFIG5_BATCH:
+        cases += [(p, g, 0, True) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
     big = None
-    for prec, algo, win in cases:
-        if prec == a.precision and algo == a.algo and win == a.window:
+    for prec, algo, win, on_big in cases:
+        if prec == a.precision and algo == a.algo and win == a.window and not on_big:
             continue
-        if win:
+        if on_big:
             if big is None:   # config 5's batch, once for the three windowed modes
                 B5 = CONFIG5_BATCH
                 codec.synth_seek(0)
@@ -516,9 +519,10 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         c.close()
         errs = int((b != ub).sum().item())
         del x
-        key = f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else "")
-        res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B,
-                    "config": "5" if win else ("3" if algo == "maxlog" and prec == "f64" else None),
+        key = f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else (f"_B{B}" if on_big else ""))
+        cfg = "5" if win else ("4 (one GPU's shard)" if on_big and prec == "f64" and algo == "logmap"
+                               else ("3" if algo == "maxlog" and prec == "f64" else None))
+        res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B, "config": cfg,
                     "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
     if big is not None and a.K == 6144:
         res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
