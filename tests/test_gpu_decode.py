@@ -186,6 +186,32 @@ def test_full_size_config2_round_trip():
         assert int((b2 != u_d).sum().item()) == 0, (algo, prec)
 
 
+def test_full_size_f32_large_batch(monkeypatch):
+    """Config 4's per-GPU shard size in fp32 (B = 32768, K = 6144, 8 iterations, 1.0 dB, the
+    device generator's frames of srand(20261015)): the occupancy pick runs four workgroups per CU
+    (turbo_decode_kernel4); its hard bits equal the two-per-CU kernel's (TD_OCC3=0) and recover
+    every info bit, in log-MAP and Max-Log-MAP."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    B, K, f1, f2 = 32768, 6144, 263, 480
+    with TurboCodec(K, f1, f2, iterations=8) as g:
+        g.synth_seed(20261015)
+        u, llr = g.synth(B, 1.0)
+        torch.cuda.synchronize()
+    x = llr.float()
+    del llr
+    for algo in ("logmap", "maxlog"):
+        out = {}
+        for occ in ("1", "0"):
+            monkeypatch.setenv("TD_OCC3", occ)
+            with TurboCodec(K, f1, f2, iterations=8, algo=algo, precision="f32") as c:
+                out[occ] = c.decode(x)
+                torch.cuda.synchronize()
+        assert torch.equal(out["1"], out["0"]), algo
+        assert int((out["1"] != u).sum().item()) == 0, algo
+
+
 def test_le_dump_layout_against_golden():
     """td_decode_device's Le dump ([B][iters][2][K+3]) and all-iteration bits on a golden frame."""
     d = np.load(os.path.join(GOLD, "frames_K1024_e0.5_s11.npz"))
