@@ -68,8 +68,9 @@ int td_reserve(td_handle* h, int B);
  * kernel's speed depends on the physical pages behind it (two modes 6-7 % apart on MI355X; the
  * slow one shows 5-8x the DRAM credit stalls), so it times one iteration on candidate workspaces
  * and keeps the fastest.  Up to TD_PLACEMENT_TRIALS candidates (environment variable, default 24;
- * 1 = a plain allocation); the search stops once one candidate runs >= 4 % below the median of
- * those timed (at least three), never on a slow straggler.  Transient memory: every candidate is
+ * 1 = a plain allocation); after at least TD_PLACEMENT_MIN candidates (default 8) the search
+ * stops once one candidate runs >= 4 % below the median of those timed, never on a slow
+ * straggler.  Transient memory: every candidate is
  * held until the choice (so each gets fresh pages), at most half the free device memory and at
  * most 144 GiB in total (config 2: ~2.4 GiB a candidate; a 32768-codeword batch: ~19 GiB).
  * Results do not depend on it.

@@ -48,9 +48,10 @@ int main()
         for (unsigned long long draws : {0ull, 1ull, 6146ull, 123456789ull}) CHECK(td_rand_window(seed, draws, win) == TD_OK);
     CHECK(td_rand_window(1, 1, nullptr) == TD_EINVAL);
     const float slow[] = {2.39f, 2.38f, 2.38f, 2.38f, 2.40f, 2.38f, 2.49f};
-    const float fast[] = {2.39f, 2.38f, 2.22f};
+    const float fast[] = {2.39f, 2.38f, 2.28f, 2.40f, 2.39f, 2.29f, 2.40f, 2.22f};
     CHECK(td_debug_placement_rule(slow, 7) == 0);
-    CHECK(td_debug_placement_rule(fast, 3) == 1);
+    CHECK(td_debug_placement_rule(fast, 3) == 0);   // fewer than TD_PLACEMENT_MIN (8) candidates
+    CHECK(td_debug_placement_rule(fast, 8) == 1);
     CHECK(td_debug_placement_rule(nullptr, 3) == TD_EINVAL);
     // argument checks: no device is touched for bad parameters
     td_handle* h = nullptr;

@@ -252,9 +252,25 @@ def test_multi_gpu_example_builds(tmp_path):
     ([2.2895, 2.2386, 2.2215, 2.2343, 2.2303], 0),                  # fast mode only: keep looking
     ([2.2895, 2.2386, 2.2215, 2.2343, 2.3797, 2.4022, 2.3166], 1),  # ... until the slow mode shows thrice
 ])
-def test_placement_stop_rule(ms, stop):
+def test_placement_stop_rule(ms, stop, monkeypatch):
     """td_reserve's placement search stops only once the fast mode is evident (td_api.cpp
-    placement_fast_seen): never on a slow straggler."""
+    placement_fast_seen): never on a slow straggler.  (The mode rule alone: TD_PLACEMENT_MIN=3.)"""
     import ctypes as C
+    monkeypatch.setenv("TD_PLACEMENT_MIN", "3")
+    arr = (C.c_float * len(ms))(*ms)
+    assert N.lib().td_debug_placement_rule(arr, len(ms)) == stop
+
+
+@pytest.mark.parametrize("ms,stop", [
+    ([2.3927, 2.3856, 2.2803], 0),                                  # round 3: a middle level, 3 probed
+    ([2.3927, 2.3856, 2.2803, 2.4011, 2.3902, 2.2876, 2.3957], 0),  # seven: not yet
+    ([2.3927, 2.3856, 2.2803, 2.4011, 2.3902, 2.2876, 2.3957, 2.2308], 1),
+    ([2.3927] * 7 + [2.4883], 0),                                   # all slow + a straggler: keep looking
+])
+def test_placement_stop_rule_min_candidates(ms, stop, monkeypatch):
+    """By default the search probes at least eight candidates before either stop rule applies, so
+    a middle-level candidate (4 % below a slow median, 2 % above the fastest level) does not end it."""
+    import ctypes as C
+    monkeypatch.delenv("TD_PLACEMENT_MIN", raising=False)
     arr = (C.c_float * len(ms))(*ms)
     assert N.lib().td_debug_placement_rule(arr, len(ms)) == stop

@@ -289,10 +289,10 @@ int ensure_ws(td_handle* h, int G)
 // (hipDeviceMallocContiguous) always landed in the slow mode.  td_reserve therefore allocates
 // candidates, all held until the choice (so each one gets fresh pages), times one turbo iteration
 // on each (best of two launches; zeroed workspace, results discarded; 2.20 vs 2.32 ms in the two modes at config 2) and
-// keeps the fastest.  It stops once two candidates differ by more than 4 % (both modes seen), at
+// keeps the fastest.  It stops once the fast mode has been seen (placement_fast_seen below), at
 // TD_PLACEMENT_TRIALS candidates (environment, default 24; 1 = a plain allocation), or when the
-// next one would take the held candidates past half the free device memory.  Results never depend
-// on the placement.
+// next one would take the held candidates past the hold cap (kPlaceHoldBytes, half the free
+// device memory).  Results never depend on the placement.
 template <typename T>
 float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e0, hipEvent_t e1, int warm)
 {
@@ -339,13 +339,25 @@ float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e
 // (the slow mode confirmed three times, so the best is not merely the fast side of one straggler).
 // A slow straggler never stops the search: with every candidate in the slow mode the median is
 // slow too and nothing is 4 % below it.  (Until round 3 the rule was "two candidates differ by
-// 4 %", which an upward outlier among slow candidates satisfied.)
+// 4 %", which an upward outlier among slow candidates satisfied.)  Neither rule is tried before
+// kPlaceMin candidates: some boxes show three levels (e.g. 2.23 / 2.28-2.30 / 2.38-2.41 ms probes;
+// decodes 17.5 / 17.8-18.2 / 18.5 ms, in probe order), and a middle-level candidate is already 4 %
+// below a slow median; with eight probed, the fastest level is almost always among them.
+#ifndef TD_PLACEMENT_MIN
+#define TD_PLACEMENT_MIN 8
+#endif
+int placement_min()
+{
+    int m = TD_PLACEMENT_MIN;
+    if (const char* e = std::getenv("TD_PLACEMENT_MIN")) m = std::atoi(e);
+    return std::max(m, 3);
+}
 bool placement_fast_seen(const std::vector<float>& ms)
 {
     std::vector<float> v;
     for (float x : ms)
         if (x > 0 && x < 1e29f) v.push_back(x);
-    if (v.size() < 3) return false;
+    if ((int)v.size() < placement_min()) return false;
     std::sort(v.begin(), v.end());
     const float med = v.size() % 2 ? v[v.size() / 2] : 0.5f * (v[v.size() / 2 - 1] + v[v.size() / 2]);
     if (v.front() < 0.96f * med) return true;
