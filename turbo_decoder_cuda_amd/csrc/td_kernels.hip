@@ -178,8 +178,18 @@ constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last buc
 #ifndef TD_LUT32_F64
 #define TD_LUT32_F64 0   // fp64 table in 32 columns (fits since the table went to 29 buckets)
 #endif
+// TD_LUT_SPLIT (fp64): a row's three fields as three ds_read_b64 (2 LDS cycles each, 32 lanes per
+// cycle, conflict-free on the 32-column table) instead of ds_read2_b64 + ds_read_b64 (8 + 2 cycles:
+// ds_read2_b64 serves 16 lanes per cycle, MI355X_MICROARCH.md LDS table).  The B pass keeps the LDS
+// array busy ~70 % of its time (SQ_LDS_IDX_ACTIVE), so LDS cycles are latency for the fold chains.
+// 1: every table read; 2: the folds' (mstar / lut_pick) only.  Forces the 32-column fp64 table.
+// Measured slower (one box, 3 rounds, config 2): 17.53 ms base, 17.85 with 1, 18.50 with 2 (the
+// volatile reads also fix the fold chains' read order); default off.
+#ifndef TD_LUT_SPLIT
+#define TD_LUT_SPLIT 0
+#endif
 template <typename T>
-constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) || (TD_LUT32_F64 && sizeof(T) == 8) ? 32 : 16;
+constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) || ((TD_LUT32_F64 || TD_LUT_SPLIT) && sizeof(T) == 8) ? 32 : 16;
 template <typename T>
 constexpr int kLutElems = 2 * kLutRows * kLutCols<T>;
 
@@ -206,10 +216,28 @@ __device__ __forceinline__ LutRow lut_row(T d)
 {
     return LutRow{bucket_dev<T>(d) * 2 * kLutCols<T>};
 }
+// the row's threshold and its two values (FOLD: a fold / recompute read, see TD_LUT_SPLIT); volatile
+// keeps the three reads from being merged into a ds_read2_b64
+template <typename T, bool FOLD = false>
+__device__ __forceinline__ void lut_fields(const T* lut, int o, T& thr, T& lo, T& hi)
+{
+    if constexpr (sizeof(T) == 8 && (TD_LUT_SPLIT == 1 || (TD_LUT_SPLIT == 2 && FOLD))) {
+        typedef __attribute__((address_space(3))) const volatile T lds_t;
+        lds_t* v = (lds_t*)lut;
+        thr = v[o];
+        lo = v[o + kLutCols<T>];
+        hi = v[o + 3 * kLutCols<T>];
+    } else {
+        thr = lut[o];
+        lo = lut[o + kLutCols<T>];
+        hi = lut[o + 3 * kLutCols<T>];
+    }
+}
 template <typename T>
 __device__ __forceinline__ T lut_pick(const T* lut, LutRow r, T d)
 {
-    const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+    T thr, lo, hi;
+    lut_fields<T, true>(lut, r.o, thr, lo, hi);
     return fabs(d) >= thr ? hi : lo;
 }
 
@@ -303,8 +331,20 @@ static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 #ifndef TD_FOLD_A
 #define TD_FOLD_A 48
 #endif
+// TD_FOLD_SPLIT (log-MAP): wave A folds 64 items (both E_seq chains in each lane) and F1 -- the
+// B pass's slowest wave (stamps: 195 cycles a step against 171-176 for the others), because it
+// shares its SIMD with the other workgroup's beta -- folds the other 32 with one chain per lane
+// (temp0 in lanes 0-31, temp1 in lanes 32-63), half the instructions of a two-chain item, and
+// the two halves meet through one lane exchange (fold_item_split).  Parity-green, measured level
+// (18.69-18.77 ms against 18.69-18.77, one box, 3 rounds): F1's instruction count does not set the
+// B pass.  Default off.
+#ifndef TD_FOLD_SPLIT
+#define TD_FOLD_SPLIT 0
+#endif
 template <int ALGO>
-constexpr int kFoldA = ALGO == 0 ? TD_FOLD_A : kFoldPerWave;
+constexpr bool kFoldSplit = TD_FOLD_SPLIT != 0 && ALGO == 0;
+template <int ALGO>
+constexpr int kFoldA = ALGO == 0 ? (kFoldSplit<ALGO> ? kLanes : TD_FOLD_A) : kFoldPerWave;
 #ifndef TD_ML_FOLD_MAP
 #define TD_ML_FOLD_MAP 1   // Max-Log-MAP fold items split by recompute depth (siso_wg B pass)
 #endif
@@ -320,6 +360,8 @@ constexpr int kAvSlots = kArec ? 2 : 4;   // alpha ring: copied 3 iterations bef
 #endif
 constexpr bool kAvDirect = TD_AV_DIRECT != 0;
 static_assert(!(kAvDirect && kArec), "TD_AV_DIRECT and TD_AREC exclude each other");
+static_assert(!(TD_FOLD_SPLIT && (kAvDirect || kArec || TD_CK_PHASES_LOGMAP != 7)),
+              "TD_FOLD_SPLIT folds from the alpha ring with every row kept");
 // every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
 template <int ALGO>
 constexpr bool kFoldRows = kArec || kCkAll<ALGO>;
@@ -783,9 +825,7 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
     if constexpr (ALGO == 0) {
         h.d = h.xp - h.xs;
         const LutRow r = lut_row(h.d);
-        h.thr = lut[r.o];
-        h.lo = lut[r.o + kLutCols<T>];
-        h.hi = lut[r.o + 3 * kLutCols<T>];
+        lut_fields<T>(lut, r.o, h.thr, h.lo, h.hi);
     }
 #ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
     if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
@@ -833,9 +873,7 @@ __device__ __forceinline__ StepHalf<T> beta_issue(T beta, const StepIn<T>& in, c
     if constexpr (ALGO == 0) {
         h.d = h.xp - h.xs;
         const LutRow r = lut_row(h.d);
-        h.thr = lut[r.o];
-        h.lo = lut[r.o + kLutCols<T>];
-        h.hi = lut[r.o + 3 * kLutCols<T>];
+        lut_fields<T>(lut, r.o, h.thr, h.lo, h.hi);
     }
     return h;
 }
@@ -918,7 +956,8 @@ struct AlphaSched {
         const T d = xp - xs;
         const LutRow r = lut_row(d);
         __builtin_amdgcn_sched_barrier(0);
-        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        T thr, lo, hi;
+        lut_fields<T>(lut, r.o, thr, lo, hi);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
@@ -1013,7 +1052,8 @@ struct AlphaSchedS {
             const T d = xp - xs;
             const LutRow r = lut_row(d);
             __builtin_amdgcn_sched_barrier(0);
-            const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+            T thr, lo, hi;
+        lut_fields<T>(lut, r.o, thr, lo, hi);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
@@ -1070,7 +1110,8 @@ struct BetaSched {
         const T d = xp - xs;
         const LutRow r = lut_row(d);
         __builtin_amdgcn_sched_barrier(0);
-        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        T thr, lo, hi;
+        lut_fields<T>(lut, r.o, thr, lo, hi);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K >= 2) op[(K + 1) % 3] = beta_in<T, (K - 2) % 3>(sm, tb, K - 2, c, lc, tmw);
         __builtin_amdgcn_sched_barrier(0);
@@ -1183,7 +1224,8 @@ __device__ __forceinline__ T arec_step(T a, const StepIn<T>& in, const T* lut, c
     if constexpr (ALGO == 0) {
         const T d = xp - xs;
         const LutRow r = lut_row(d);
-        const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+        T thr, lo, hi;
+        lut_fields<T>(lut, r.o, thr, lo, hi);
         Avw[k * kLanes + rot_off<T>(lc.st_off[PH], k)] = alpha;   // behind the table read
         return sched_finish(xs, xp, d, thr, lo, hi);
     } else {
@@ -1210,7 +1252,8 @@ struct AlphaSchedR {
             const T d = xp - xs;
             const LutRow r = lut_row(d);
             __builtin_amdgcn_sched_barrier(0);
-            const T thr = lut[r.o], lo = lut[r.o + kLutCols<T>], hi = lut[r.o + 3 * kLutCols<T>];
+            T thr, lo, hi;
+        lut_fields<T>(lut, r.o, thr, lo, hi);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
@@ -1566,6 +1609,49 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const int i = i0 + k;
     if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
     if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
+}
+
+// fold_item_fast with one E_seq chain per lane (TD_FOLD_SPLIT, wave F1): lane l < 32 folds temp0 of
+// the item (fl.k, fl.c), lane l + 32 temp1 of the same item.  temp1[j] = (alpha[p1(j)] + G) + beta[j]
+// and temp0[j] = (alpha[p0(j)] - G) + beta[j] use the same G = P|Q (kTrellisQ[p0(j)] ==
+// kTrellisQ[p1(j)]) and p1(j) = p0(j) ^ 1, so the temp1 lanes read their alpha block with the two
+// states of each pair swapped and both halves run one instruction stream: fma(+-1, G, alpha) + beta
+// (fma(-1, G, a) = a - G exactly), then the chain.  Called by all 64 lanes (the exchange needs them).
+template <typename T, int ALGO>
+__device__ __forceinline__ void fold_item_split(const FoldLane<T>& fl, const T* lut, int s3, int s4, int s2, int i0,
+                                                int ext_len, int K, int u, bool active)
+{
+    const int k = fl.k;
+    const T* g = fl.G + s3 * (kW * kCw * 4);
+    const T P = g[0], Q = g[1], ys = g[2], la = g[3];
+    const int* wp = fl.Wp + s3 * (kW * 2);
+    const int wperm = wp[0], wbit = wp[1];
+    T a[8], b[8], t[8];
+    load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
+    // alpha state s ^ u into a[s], read at its own address (the pair's two states are adjacent in
+    // the block: blk_off(s ^ 1) = blk_off(s) ^ 1); u opaque, so the compiler reads, not selects
+    int ux = u;
+    touch(ux);
+    const T* av = fl.Av + s4 * (kW * kLanes);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = av[blk_off<T>(q, k) ^ ux];
+    const T sg = u ? (T)1 : (T)-1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0];
+        t[j] = fma(sg, kTrellisQ[p0] ? Q : P, a[p0]) + b[j];   // a[p0] = alpha[p1(j)] in the temp1 lanes
+    }
+    T r = mstar<T, ALGO>(t[0], t[1], lut);
+#pragma unroll
+    for (int j = 2; j < 8; ++j) r = mstar<T, ALGO>(r, t[j], lut);
+    const T r1 = __shfl_xor(r, 32);   // lanes l < 32: temp1's fold from lane l + 32
+    if (u == 0 && active) {
+        const T llr = r1 - r;
+        const T le = llr - la - (T)2 * ys;
+        const int i = i0 + k;
+        if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
+        if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
+    }
 }
 
 #ifdef TD_STAMPS
@@ -1971,8 +2057,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 TD_ACC(3, b1, b2);
             }
             FoldLane<T> fl;
-            fl.k = fe >> 3;
-            fl.c = fe & 7;
+            const bool f1split = kFoldSplit<ALGO> && wave != 0;   // F1: one chain per lane (fold_item_split)
+            const int fes = f1split ? kFoldA<ALGO> + (lane & 31) : fe;
+            fl.k = fes >> 3;
+            fl.c = fes & 7;
             const int ke = min(fl.k, kW - 1);   // spare lanes: any valid row (they fold nothing)
             fl.G = &sm.G[0][ke][fl.c][0];
             fl.Wp = &sm.Wp[0][ke][0];
@@ -1993,7 +2081,24 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
-            for (int j = 3; j < nB; ++j, --wf) {
+            if constexpr (kFoldSplit<ALGO>) {
+                if (f1split) {   // F1, one chain per lane: its own loop (one instruction stream per role)
+                    const int u = lane >> 5;
+                    for (int j = 3; j < nB; ++j, --wf) {
+                        TD_STAMP(b0);
+                        fold_item_split<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K, u, true);
+                        s3 = s3 == 0 ? 2 : s3 - 1;
+                        s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
+                        s2 ^= 1;
+                        TD_STAMP(b1);
+                        wg_sync_lds();
+                        TD_STAMP(b2);
+                        TD_ACC(2, b0, b1);
+                        TD_ACC(3, b1, b2);
+                    }
+                }
+            }
+            for (int j = 3; j < nB && !(kFoldSplit<ALGO> && f1split); ++j, --wf) {
                 TD_STAMP(b0);
                 T afar[8];
                 if constexpr (kAvDirect) load_block_global<T>(ag + (size_t)max(wf - 2, 0) * aws, afar);
