@@ -12,7 +12,7 @@ for v in $VARIANTS; do
   flags=${v#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-honor-nans \
     -Iinclude -I$PKG/csrc ${flags//,/ } -shared -o $PKG/libvar_$name.so \
-    $PKG/csrc/td_kernels.hip $PKG/csrc/td_synth.hip $PKG/csrc/td_api.cpp &
+    $PKG/csrc/td_kernels.hip $PKG/csrc/td_kernels_w12.hip $PKG/csrc/td_synth.hip $PKG/csrc/td_api.cpp &
 done
 wait
 ls -la $PKG/libvar_*.so

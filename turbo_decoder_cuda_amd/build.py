@@ -58,7 +58,7 @@ def _run_hip(cmd, verbose):
 
 
 def build(force: bool = False, verbose: bool = False) -> None:
-    srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_synth.hip", "td_api.cpp")]
+    srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_kernels_w12.hip", "td_synth.hip", "td_api.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
     if force or _newer(LIB, deps):
         _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-shared", "-o", LIB, *srcs], verbose)

@@ -29,7 +29,7 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
-constexpr int kPermPad = 16;         // spare ints after pi / pinv: the loader stages window-sized chunks
+constexpr int kPermPad = 32;         // spare ints after pi / pinv: the loader stages window-sized chunks
 // TD_AREC: alpha recomputed in the B pass by a fifth wave per codeword group (td_kernels.hip)
 #ifndef TD_AREC
 #define TD_AREC 0
@@ -52,7 +52,12 @@ constexpr size_t astore_group_elems(int L) { return (size_t)L * 64 + TD_APAD; }
 #ifndef TD_AWIN
 #define TD_AWIN 0
 #endif
-constexpr int kWindowSteps = 12;   // td_kernels.hip kW
+// Trellis steps per window of the exact schedule (td_kernels.hip kW): a multiple of 3 (the label
+// period) with at most 128 (step, codeword) fold items (two fold waves, one item per lane), so 12 or 15.
+#ifndef TD_KW
+#define TD_KW 15
+#endif
+constexpr int kWindowSteps = TD_KW;   // td_kernels.hip kW
 constexpr int awin_windows(int L) { return (L + kWindowSteps - 1) / kWindowSteps; }
 constexpr size_t astore_elems(int G, int L)
 {
@@ -106,6 +111,10 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 // the turbo iterations (one wave per 8 codewords)
 template <typename T>
 hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st, bool probe = false);   // probe: td_reserve's placement probe symbol
+// fp32 at four workgroups per CU, from td_kernels_w12.hip (td_kernels.hip built with 12-step windows,
+// whose fp32 LDS fits four per CU; the default 15-step windows fit three)
+template <typename T, int ALGO>
+hipError_t launch_turbo4_w12(const DecodeParams<T>& p, hipStream_t st);
 
 // sliding-window mode (BASELINE config 5, td_set_window): sub-blocks of `window` steps
 struct WindowParams {

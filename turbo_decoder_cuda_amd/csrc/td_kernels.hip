@@ -36,9 +36,18 @@
 #include "td_kernels.h"
 #include "td_tables.h"
 
+// td_kernels_w12.hip compiles this file a second time with 12-step windows (TD_W12_TU) into its own
+// namespace, for the one launch that needs them: fp32 at four workgroups per CU (launch_turbo4_w12).
+#ifdef TD_W12_TU
+namespace td_w12 {
+using namespace ::td;
+#else
 namespace td {
+#endif
 
-constexpr int kW = 12;                          // steps per window (multiple of 3)
+constexpr int kW = kWindowSteps;                // steps per window (multiple of 3; td_kernels.h TD_KW)
+static_assert(kW == 12 || kW == 15, "windows of 12 or 15 steps");
+constexpr int kArow0 = kW / 2;                  // scheduled alpha stores: rows addressed from row kArow0 (immediates)
 constexpr int kCw = 8;                          // codewords per workgroup
 constexpr int kLanes = 64;
 constexpr int kTile = kW * kCw;                 // (step, codeword) elements per window
@@ -329,7 +338,7 @@ static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
 // log-MAP: fold items of wave A (its SIMD partner is the other workgroup's loader) per window; F1,
 // which shares its SIMD with the other workgroup's beta, takes the remaining kTile - kFoldA
 #ifndef TD_FOLD_A
-#define TD_FOLD_A 48
+#define TD_FOLD_A (kTile / 2)
 #endif
 // TD_FOLD_SPLIT (log-MAP): wave A folds 64 items (both E_seq chains in each lane) and F1 -- the
 // B pass's slowest wave (stamps: 195 cycles a step against 171-176 for the others), because it
@@ -371,11 +380,16 @@ constexpr bool kFoldRows = kArec || kCkAll<ALGO>;
 // loader then converts a landed slot into the ring.  A staged window is 16-byte chunks: ys, yp, La
 // ([kW][8] each), then the write positions pi-or-pinv[kW] and pi[kW]; spare lanes land past them.
 constexpr int kDmaBytes = kLanes * 16;   // one DMA instruction
-static_assert(kW % 4 == 0, "a window's write positions are whole 16-byte chunks");
+
 template <typename T>
 constexpr int kStreamChunks = kTile * (int)sizeof(T) / 16;   // chunks of one [kW][8] stream
+// write positions: a window's kW ints of each table from the 16-byte-aligned chunk at or below its
+// first step (kW = 12: always aligned, 3 chunks; 15: start offset (15 t) mod 4, 5 chunks)
+constexpr int kWpChunks = kW % 4 == 0 ? kW / 4 : (kW + 3 + 3) / 4;
+constexpr int kWpInts = 4 * kWpChunks;   // staged ints per table
+static_assert(kW % 4 == 0 || kWpInts >= kW + 3, "a window's write positions lie within its staged chunks");
 template <typename T>
-constexpr int kTileChunks = 3 * kStreamChunks<T> + 2 * (kW / 4);
+constexpr int kTileChunks = 3 * kStreamChunks<T> + 2 * kWpChunks;
 template <typename T>
 constexpr int kTileDma = (kTileChunks<T> + kLanes - 1) / kLanes;   // DMA instructions per staged window
 // Staging slots hold exactly a window's chunks: the last DMA of a window (and the tempmax DMA) run on
@@ -390,10 +404,10 @@ struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][2];          // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
-    T Av[kAvDirect ? 1 : kAvSlots][kAvDirect ? 1 : kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state
+    alignas(16) T Av[kAvDirect ? 1 : kAvSlots][kAvDirect ? 1 : kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state
                                                                     // (fold input, DMA from HBM; unused: TD_AV_DIRECT)
-    T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
-    T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
+    alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
+    alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
     alignas(16) unsigned char stage[3][kStageBytes<T>];     // loader: staged window inputs
     alignas(16) unsigned char tmstage[3][kTmStageBytes<T>];  // loader: staged tempmax of a window
 };
@@ -595,7 +609,8 @@ __device__ __forceinline__ void dma16_s(unsigned lds, const void* sbase, unsigne
 // Stage window t (rows clamped into range, so the count of DMA instructions never varies; values
 // are masked where they are converted).  Every read is sequential: the interleaver permutations
 // are applied when the extrinsic is WRITTEN (fold), so no load address depends on another load.
-// The write-position chunks read up to 13 ints past K: the permutation tables carry 16 spare ints.
+// The write-position chunks read up to kMemory + kWpInts - 1 ints past K - 1: the permutation tables
+// carry kPermPad spare ints.
 template <typename T>
 __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>& src, const SisoDst<T>& dst,
                                          const Geom& gm, int t, int lane)
@@ -618,10 +633,11 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const size_t sb = a0 + (size_t)(s == 1) * (a1 - a0) + (size_t)(s == 2) * (a2 - a0);
         const size_t row = s == 2 ? (size_t)gm.g * src.la_cap + min(i, src.la_cap - 1) : (size_t)gm.g * gm.L + i;
         const char* ps = reinterpret_cast<const char*>(sb + (row * kCw + (e0 & 7)) * sizeof(T));
-        // write-position chunks: r < kW/4 pi-or-pinv, else pi
-        const int r = min(max(ch - 3 * nc, 0), 2 * (kW / 4) - 1);
-        const int* pb = r < kW / 4 ? pperm : gm.pi;
-        const char* pw = reinterpret_cast<const char*>(pb + tc * kW + (r % (kW / 4)) * 4);
+        // write-position chunks: r < kWpChunks pi-or-pinv, else pi; from the aligned chunk at or
+        // below the window's first step
+        const int r = min(max(ch - 3 * nc, 0), 2 * kWpChunks - 1);
+        const int* pb = r < kWpChunks ? pperm : gm.pi;
+        const char* pw = reinterpret_cast<const char*>(pb + ((tc * kW) & ~3) + (r % kWpChunks) * 4);
         if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
             dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
     }
@@ -659,7 +675,7 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
     const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
     const T* sp = sy + kTile;
     const T* sl = sy + 2 * kTile;
-    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile);   // [kW] pi-or-pinv, then [kW] pi
+    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);   // [kWpInts] pi-or-pinv, then [kWpInts] pi
     T* g = &sm.G[t % 3][0][0][0];
     int* w = &sm.Wp[t % 3][0][0];
 #pragma unroll
@@ -676,14 +692,14 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
             g[4 * e + 3] = la;
             if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
                 w[2 * k] = sw[k];
-                w[2 * k + 1] = sw[kW + k];
+                w[2 * k + 1] = sw[kWpInts + k];
             }
         }
     }
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
-static_assert(kMemory + kW - 2 < kPermPad, "write-position chunks stay within the padded tables");
+static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
 
 // ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
 // Scratch layout: alpha by 8c + state in windows of kW rows (astore_window_off: window-major
@@ -725,7 +741,13 @@ __device__ __forceinline__ int ck_row_of(int k, int& ks)
 template <typename T, int ALGO>
 constexpr int alpha_dma_count()
 {
-    return (kAvDirect || kArec) ? 0 : kCkRows<ALGO> * kLanes * (int)sizeof(T) / (kLanes * 16);
+    return (kAvDirect || kArec) ? 0 : (kCkRows<ALGO> * kLanes * (int)sizeof(T) + kDmaBytes - 1) / kDmaBytes;
+}
+// bytes of a window's stored alpha rows (the last DMA covers the lanes below it only)
+template <typename T, int ALGO>
+constexpr int alpha_dma_bytes()
+{
+    return kCkRows<ALGO> * kLanes * (int)sizeof(T);
 }
 static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
@@ -757,7 +779,8 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
         }
         const int s0 = ck_step<ALGO>(q * rpd);   // source step of the DMA's first row
         const int sr = ck_step<ALGO>(r);
-        dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
+        if (q + 1 < n || q * kDmaBytes + lane * 16 < alpha_dma_bytes<T, ALGO>())
+            dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
     }
 #else   // round-2 form: a 64-bit per-lane source pointer per DMA (contiguous rows only)
     static_assert(TD_AWIN != 2, "the per-lane form assumes contiguous window rows");
@@ -771,7 +794,7 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
             off = ck_step<ALGO>(r) * row_bytes + (w / blk) * blk + pc * 16;
         }
-        dma16(lds + q * kDmaBytes, src + off);
+        if (q + 1 < n || b < alpha_dma_bytes<T, ALGO>()) dma16(lds + q * kDmaBytes, src + off);
     }
 #endif
 }
@@ -979,9 +1002,12 @@ struct AlphaSched<T, kW> {
 // AlphaSched for a full window t >= 1 with its scratch stores addressed off wave-uniform bases
 // (TD_SADDR): sa = alpha rows of the window + 6 rows, stm = tempmax rows of the window; va[PH] =
 // this lane's byte offset of its state in a row of phase PH, vtm = its codeword's.  Step K stores
-// alpha at sa + va + (K - 6) rows and tempmax[i] at scratch index i - 1 = stm + vtm + (K - 1) rows.
+// alpha at sa + va + (K - kArow0) rows and tempmax[i] at scratch index i - 1 = stm + vtm + (K - 1) rows.
 #ifndef TD_SADDR
 #define TD_SADDR 1
+#endif
+#ifndef TD_LOADER_PRIO_B
+#define TD_LOADER_PRIO_B 0   // VALU priority of the loader wave in the log-MAP B pass
 #endif
 #ifndef TD_LOADER_PRIO_MAXLOG
 #define TD_LOADER_PRIO_MAXLOG 0   // VALU priority of the loader wave in the Max-Log-MAP B pass
@@ -995,13 +1021,15 @@ struct AlphaSched<T, kW> {
                             // it keeps alpha_window's pinned step groups
 #endif
 // TD_TM_BATCH: the 8 lanes of a codeword hold the same tempmax, so instead of a store per step each
-// lane keeps the tempmax of one step (lane slot l: steps l and 8 + (l & 3) of the window) and the
-// window writes them with two stores (steps 0-7, then 8-11; lanes l and l + 4 write the same value
-// twice in the second): 2 scratch stores a window instead of 12 beside the recursion.
+// lane keeps the tempmax of one step (lane slot l: steps l and 8 + tm2_slot(l) of the window) and
+// the window writes them with two stores (steps 0-7, then 8..kW-1; lanes whose slots map to one
+// step write the same value twice in the second): 2 scratch stores a window instead of kW.
 #ifndef TD_TM_BATCH
 #define TD_TM_BATCH 1
 #endif
-static_assert(kW == 12, "the tempmax batches cover a window of 8 + 4 steps");
+static_assert(kW > 8 && kW <= 16, "the tempmax batches cover a window of 8 + (kW - 8) steps");
+// the second batch's step (minus 8) kept by lane slot l
+__host__ __device__ constexpr int tm2_slot(int l) { return kW - 8 == 4 ? (l & 3) : (l < kW - 8 ? l : kW - 9); }
 template <typename T>
 struct TmBatch {
     T buf;
@@ -1015,16 +1043,16 @@ __device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm, unsigned v
         if constexpr (K < 8)
             tbh.buf = tbh.slot == K ? m : tbh.buf;
         else
-            tbh.buf = (tbh.slot & 3) == K - 8 ? m : tbh.buf;
+            tbh.buf = tm2_slot(tbh.slot) == K - 8 ? m : tbh.buf;
         if constexpr (K == 7) gstore_s<-kCw * (int)sizeof(T)>(stm, tbh.v1, tbh.buf);           // steps 0-7 at i - 1
-        if constexpr (K == kW - 1) gstore_s<7 * kCw * (int)sizeof(T)>(stm, tbh.v2, tbh.buf);   // steps 8-11
+        if constexpr (K == kW - 1) gstore_s<7 * kCw * (int)sizeof(T)>(stm, tbh.v2, tbh.buf);   // steps 8..kW-1
     } else {
         gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);   // tempmax[i] at scratch index i - 1
     }
 }
 
 // alpha row K of a full window: wave-uniform base sa in SGPRs, per-lane byte offset voff.  Window-
-// and group-major layouts (TD_AWIN 0, 1): sa = row 6 of the window and the row is an immediate offset
+// and group-major layouts (TD_AWIN 0, 1): sa = row kArow0 of the window and the row is an immediate offset
 // (no per-step address arithmetic); step-major (TD_AWIN 2): sa = row 0, rows arow elements apart.
 template <typename T, int K>
 __device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v, size_t arow)
@@ -1032,7 +1060,7 @@ __device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v, size_t aro
     if constexpr (TD_AWIN == 2)
         gstore_s<0>(sa + K * arow, voff, v);
     else
-        gstore_s<(K - 6) * kLanes * (int)sizeof(T)>(sa, voff, v);
+        gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
 }
 
 template <typename T, int ALGO, int K>
@@ -1085,7 +1113,7 @@ struct AlphaSchedS<T, ALGO, kW> {
     {
     }
 };
-static_assert(6 * kLanes * 8 <= 4096 && (kW - 7) * kLanes * 8 < 4096, "scheduled alpha store offsets fit the immediate");
+static_assert(kArow0 * kLanes * 8 <= 4096 && (kW - 1 - kArow0) * kLanes * 8 < 4096, "scheduled alpha store offsets fit the immediate");
 
 // TD_BETA_SHADOW: each beta step writes its incoming beta[.][i+1] (the fold input of step i) into
 // the window's Bv rows behind its own row read, instead of the 12 writes (and their rotated
@@ -1674,14 +1702,15 @@ __device__ __forceinline__ void fold_item_split(const FoldLane<T>& fl, const T* 
 // TD_ROLE_REMAT: the lane index made opaque at the start of every SISO, so that the compiler cannot
 // hoist the roles' lane-derived addresses (fold lanes, alpha store offsets, ...) out of the SISO loop,
 // where they were all live at once, in every role: fp64 log-MAP 256 -> 95 VGPRs, fp32 log-MAP 191 ->
-// 78, so that three workgroups fit a CU (turbo_decode_kernel3).  1 (default): fp32 only -- at two
+// 78, so that three workgroups fit a CU (turbo_decode_kernel3).  1 (default): fp32, and fp64 with
+// 15-step windows (without it that build spills to scratch) -- with 12-step windows at two
 // workgroups per CU it measured level in fp64 log-MAP (17.39 vs 17.40 ms) and 1.4 % slower in fp64
 // Max-Log-MAP; 2: both precisions; 0: off.
 #ifndef TD_ROLE_REMAT
 #define TD_ROLE_REMAT 1
 #endif
 template <typename T>
-constexpr bool kRoleRemat = TD_ROLE_REMAT == 2 || (TD_ROLE_REMAT == 1 && sizeof(T) == 4);
+constexpr bool kRoleRemat = TD_ROLE_REMAT == 2 || (TD_ROLE_REMAT == 1 && (sizeof(T) == 4 || kW != 12));
 constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
                                  // barriers, F prologue, loader B prologue, loader first tile (see diag)
@@ -1748,8 +1777,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                         (unsigned)(lc.st_off[2] * sizeof(T))};
                 const unsigned vtm = (unsigned)(c * sizeof(T));
                 TmBatch<T> tbh{(T)0, lane & 7, (unsigned)(((lane & 7) * kCw + c) * sizeof(T)),
-                               (unsigned)(((lane & 3) * kCw + c) * sizeof(T))};
-                T* sa = ga0 + aws + (TD_AWIN == 2 ? 0 : (size_t)6 * kLanes);   // window 1, row 6 (row 0: astore_row)
+                               (unsigned)((tm2_slot(lane & 7) * kCw + c) * sizeof(T))};
+                T* sa = ga0 + aws + (TD_AWIN == 2 ? 0 : (size_t)kArow0 * kLanes);   // window 1, row kArow0 (row 0: astore_row)
                 T* stm = gtm0 + (size_t)kW * kCw;
                 const T* lut = lut_col(sm, lane);
                 unsigned long long* chain_st = st ? st + 4 : nullptr;
@@ -1849,6 +1878,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
         if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
+        if constexpr (ALGO == 0 && TD_LOADER_PRIO_B) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_B);
         auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
 #if TD_LOADER_REMAT
@@ -2019,7 +2049,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
         int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
-        if constexpr (!kFoldRows<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP)) {
+        if constexpr (!kFoldRows<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP) && kTile - kTile / 3 <= kLanes) {
+            // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
             // takes the 32 items of the phase furthest from a kept row (pd), the fold wave beside
             // the other workgroup's beta (F1) the 64 items of the other two phases.  Max-Log-MAP
@@ -2354,6 +2385,14 @@ __global__ __launch_bounds__(kWaves * 64, kArec ? 4 : 3) void turbo_decode_kerne
 template <typename T, int ALGO>
 constexpr bool kOcc4 = TD_OCC4 != 0 && !kArec && kGroupsPerWg == 1 && 4 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
                        kRoleRemat<T>;
+// fp32 four per CU from the 12-step-window build when this one's Smem does not fit four (launch_turbo4_w12)
+#ifdef TD_W12_TU
+template <typename T, int ALGO>
+constexpr bool kOcc4W12 = false;
+#else
+template <typename T, int ALGO>
+constexpr bool kOcc4W12 = TD_OCC4 != 0 && !kOcc4<T, ALGO> && sizeof(T) == 4 && kW != 12 && !kArec && kGroupsPerWg == 1;
+#endif
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kWaves * 64, 4) void turbo_decode_kernel4(DecodeParams<T> p)
 {
@@ -2886,7 +2925,8 @@ template <typename T, int ALGO>
 int occupancy_pick(const DecodeParams<T>& p)
 {
     if (!p.occ3 || p.role_cus <= 0 || p.G <= 2 * p.role_cus) return 2;
-    const double t_rel[5] = {1.0, 1.0, 1.0, ALGO == 1 ? 1.07 : 1.17, ALGO == 1 ? 1.29 : 1.39};
+    // (four per CU run the 12-step-window build: relative to two per CU with 15-step windows, 1.42)
+    const double t_rel[5] = {1.0, 1.0, 1.0, ALGO == 1 ? 1.07 : 1.17, kW == 12 ? (ALGO == 1 ? 1.29 : 1.39) : 1.42};
     auto est = [&](int n) {
         const long per_round = (long)n * p.role_cus;
         const long full = p.G / per_round, rem = p.G % per_round;
@@ -2895,8 +2935,17 @@ int occupancy_pick(const DecodeParams<T>& p)
     };
     int best = 2;
     if (kOcc3<T, ALGO> && est(3) < est(best)) best = 3;
-    if (kOcc4<T, ALGO> && est(4) < est(best)) best = 4;
+    if ((kOcc4<T, ALGO> || kOcc4W12<T, ALGO>) && est(4) < est(best)) best = 4;
     return best;
+}
+
+template <typename T, int ALGO>
+hipError_t launch_kernel4(const DecodeParams<T>& p, hipStream_t st)
+{
+    hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel4<T, ALGO>), sizeof(Smem<T>));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((turbo_decode_kernel4<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
+    return hipGetLastError();
 }
 
 template <typename T, int ALGO>
@@ -2904,10 +2953,11 @@ hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool prob
 {
     const int occ = probe ? 2 : occupancy_pick<T, ALGO>(p);
     if (occ == 4) {
-        hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel4<T, ALGO>), sizeof(Smem<T>));
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((turbo_decode_kernel4<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), sizeof(Smem<T>), st, p);
-        return hipGetLastError();
+        if constexpr (kOcc4<T, ALGO>) return launch_kernel4<T, ALGO>(p, st);
+#ifndef TD_W12_TU
+        else if constexpr (kOcc4W12<T, ALGO>) return launch_turbo4_w12<T, ALGO>(p, st);
+#endif
+        else return hipErrorInvalidConfiguration;
     }
     if (occ == 3) {
         hipError_t e = allow_smem(reinterpret_cast<const void*>(&turbo_decode_kernel3<T, ALGO>), wg_lds3<T>());
@@ -2975,6 +3025,7 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
     return hipGetLastError();
 }
 
+#ifndef TD_W12_TU
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t, bool);
@@ -2991,5 +3042,21 @@ template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*,
 int window_steps() { return kW; }
 static_assert(kW == kWindowSteps, "td_kernels.h kWindowSteps is the kernel's window");
 int groups_per_wg() { return kGroupsPerWg; }
+#endif
 
+}  // namespace td / td_w12
+
+#ifdef TD_W12_TU
+namespace td {
+template <typename T, int ALGO>
+hipError_t launch_turbo4_w12(const DecodeParams<T>& p, hipStream_t st)
+{
+    static_assert(td_w12::kOcc4<T, ALGO>, "the 12-step-window build has the four-per-CU kernel");
+    DecodeParams<T> q = p;
+    q.nT = (q.L + td_w12::kW - 1) / td_w12::kW;   // windows of this build
+    return td_w12::launch_kernel4<T, ALGO>(q, st);
+}
+template hipError_t launch_turbo4_w12<float, 0>(const DecodeParams<float>&, hipStream_t);
+template hipError_t launch_turbo4_w12<float, 1>(const DecodeParams<float>&, hipStream_t);
 }  // namespace td
+#endif
