@@ -1888,12 +1888,22 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             const int wa = tl - j;
             if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
             if (wa >= 0) tm_convert(sm, slot, wa, lane);
+#ifdef TD_STAMPS_LOADER   // diagnostic split of the loader's B-pass work (slots 11: converts, 13: their drain)
+            TD_STAMP(bc);
+            TD_ACC(11, b0, bc);
+#endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+#ifdef TD_STAMPS_LOADER
+            TD_STAMP(bl);
+            TD_ACC(13, bc, bl);
+#endif
             tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
             tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
             alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+            TD_STAMP(bw);
             vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
             TD_STAMP(b1);
+            TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
             wg_sync_lds();
             TD_STAMP(b2);
             TD_ACC(2, b0, b1);
