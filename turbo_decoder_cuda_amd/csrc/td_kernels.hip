@@ -698,6 +698,80 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
     }
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
+
+// tile_convert (TILE) and tm_convert (TM) of one B-pass iteration with every LDS read issued before
+// the first write: written as two functions, each pass's reads waited for the previous pass's
+// writes (the compiler cannot tell the staging slots from the rings), four dependent LDS round trips
+// per window -- ~108 cycles a step of the loader's ~170, which sets the B pass with 15-step windows.
+#ifndef TD_CONVERT_BATCH
+#define TD_CONVERT_BATCH 0   // measured level (17.20-17.26 vs 17.25-17.28 ms, one box, 3 rounds): off
+#endif
+template <typename T>
+__device__ __forceinline__ void bpass_convert(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int lane, bool tile,
+                                              bool tm)
+{
+    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
+    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);
+    const T* sv = reinterpret_cast<const T*>(&sm.tmstage[slot][0]);
+    T ys[2], yp[2], la[2], tv[2];
+    int w0 = 0, w1 = 0;
+    const int k0 = lane >> 3;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = min(lane + kLanes * q, kTile - 1);
+        if (tile) {
+            ys[q] = sy[e];
+            yp[q] = sy[kTile + e];
+            la[q] = sy[2 * kTile + e];
+        }
+        if (tm) tv[q] = sv[e];
+    }
+    if (tile && (lane & 7) == 0) {
+        w0 = sw[min(k0, kW - 1)];
+        w1 = sw[kWpInts + min(k0, kW - 1)];
+    }
+    int w0b = 0, w1b = 0;
+    if (tile && (lane & 7) == 0 && k0 + 8 < kW) {
+        w0b = sw[k0 + 8];
+        w1b = sw[kWpInts + k0 + 8];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // every read above is in flight before any write below
+    if (tile) {
+        T* g = &sm.G[t % 3][0][0][0];
+        int* w = &sm.Wp[t % 3][0][0];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int e = lane + kLanes * q;
+            if (e < kTile) {
+                const int k = e >> 3;
+                const T l = la_at(src, t * kW + k, la[q]);
+                const T hla = l / (T)2;
+                g[4 * e] = (ys[q] + yp[q]) + hla;
+                g[4 * e + 1] = (ys[q] - yp[q]) + hla;
+                g[4 * e + 2] = ys[q];
+                g[4 * e + 3] = l;
+            }
+        }
+        if ((lane & 7) == 0) {   // one entry per step: every codeword has the same positions
+            if (k0 < kW) {
+                w[2 * k0] = w0;
+                w[2 * k0 + 1] = w1;
+            }
+            if (k0 + 8 < kW) {
+                w[2 * (k0 + 8)] = w0b;
+                w[2 * (k0 + 8) + 1] = w1b;
+            }
+        }
+    }
+    if (tm) {
+        T* d = &sm.tm[t & 1][0][0];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int e = lane + kLanes * q;
+            if (e < kTile) d[e] = tv[q];
+        }
+    }
+}
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
 
@@ -1886,8 +1960,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             touch(lane);
 #endif
             const int wa = tl - j;
-            if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
-            if (wa >= 0) tm_convert(sm, slot, wa, lane);
+            if constexpr (TD_CONVERT_BATCH != 0) {
+                if (wa >= 0) bpass_convert(sm, slot, src, wa, lane, wa <= tl - 3, true);
+            } else {
+                if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
+                if (wa >= 0) tm_convert(sm, slot, wa, lane);
+            }
 #ifdef TD_STAMPS_LOADER   // diagnostic split of the loader's B-pass work (slots 11: converts, 13: their drain)
             TD_STAMP(bc);
             TD_ACC(11, b0, bc);
