@@ -1948,7 +1948,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // (last read at j-1).  All DMAs are unconditional (clamped windows, a spare slot at the
         // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
         // own and the previous iteration's DMAs in flight: three windows of latency for each.
-        constexpr int kB = kF + 1 + alpha_dma_count<T, ALGO>();
+#ifdef TD_DIAG_NOADMA   // diagnostics only (wrong results): the B pass without the loader's alpha copies
+        constexpr int kAd = 0;
+#else
+        constexpr int kAd = alpha_dma_count<T, ALGO>();
+#endif
+        constexpr int kB = kF + 1 + kAd;
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
         if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
@@ -1960,12 +1965,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             touch(lane);
 #endif
             const int wa = tl - j;
+#ifndef TD_DIAG_NOBCONVERT   // diagnostics only (wrong results): no B-pass converts (tiles stay as staged)
             if constexpr (TD_CONVERT_BATCH != 0) {
                 if (wa >= 0) bpass_convert(sm, slot, src, wa, lane, wa <= tl - 3, true);
             } else {
                 if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 if (wa >= 0) tm_convert(sm, slot, wa, lane);
             }
+#endif
 #ifdef TD_STAMPS_LOADER   // diagnostic split of the loader's B-pass work (slots 11: converts, 13: their drain)
             TD_STAMP(bc);
             TD_ACC(11, b0, bc);
@@ -1977,7 +1984,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
 #endif
             tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
             tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
-            alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+            if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
             TD_STAMP(bw);
             vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
             TD_STAMP(b1);
@@ -1993,8 +2000,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         tm_dma(sm, 1, tmstore, gm, tl - 1, lane);
         tile_dma(sm, 2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never converted
         tm_dma(sm, 2, tmstore, gm, tl - 2, lane);
-        alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);          // folded at j = 2
-        vm_wait<2 * (kF + 1) + alpha_dma_count<T, ALGO>()>();   // slot 0 landed
+        if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);   // folded at j = 2
+        vm_wait<2 * (kF + 1) + kAd>();   // slot 0 landed
         TD_STAMP(p4);
         TD_ACC(12, p3, p4);
         for (int j = 0; j < nB; j += 3) {
