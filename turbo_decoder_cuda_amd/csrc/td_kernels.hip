@@ -830,7 +830,11 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
 {
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
+#ifdef TD_DIAG_ADMA_L2   // diagnostics only (wrong results): every copy reads window 0 of group 0 (L2-resident)
+    const char* src = reinterpret_cast<const char*>(astore);
+#else
     const char* src = reinterpret_cast<const char*>(astore + astore_window_off(gm.g, tc, gm.G, gm.L));
+#endif
     const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
