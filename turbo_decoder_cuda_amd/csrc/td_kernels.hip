@@ -561,10 +561,16 @@ __device__ __forceinline__ void gstore(float* p, float v)
 
 // the same with a wave-uniform base in SGPRs, a per-lane 32-bit byte offset and an immediate (the
 // scheduled alpha windows: no per-step 64-bit address arithmetic)
+#ifndef TD_ASTORE_NT
+#define TD_ASTORE_NT 0   // 1: the scheduled alpha / tempmax scratch stores carry nt
+#endif
 template <int IMM>
 __device__ __forceinline__ void gstore_s(double* base, unsigned voff, double v)
 {
-    asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
+    if constexpr (TD_ASTORE_NT)
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
+    else
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
 }
 template <int IMM>
 __device__ __forceinline__ void gstore_s(float* base, unsigned voff, float v)
@@ -588,6 +594,30 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
                  : "=&s"(save)
                  : "s"(lds), "v"(src)
                  : "memory");
+}
+
+// dma16 with a cache-policy suffix on the load (TD_ADMA_POLICY: the alpha copies, read once)
+#ifndef TD_ADMA_POLICY
+#define TD_ADMA_POLICY 0   // 0: none, 1: nt, 2: sc1, 3: sc0 sc1 nt
+#endif
+#ifndef TD_TDMA_POLICY
+#define TD_TDMA_POLICY 0   // the same for the tile and tempmax stagings
+#endif
+template <int POL>
+__device__ __forceinline__ void dma16_pol(unsigned lds, const void* src)
+{
+    unsigned save;
+    if constexpr (POL == 1)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
+    else if constexpr (POL == 2)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
+    else if constexpr (POL == 3)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off sc0 sc1 nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
+    else
+        dma16(lds, src);
 }
 
 // dma16 with a wave-uniform SGPR base and a per-lane 32-bit byte offset (saddr form)
@@ -639,7 +669,7 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const int* pb = r < kWpChunks ? pperm : gm.pi;
         const char* pw = reinterpret_cast<const char*>(pb + ((tc * kW) & ~3) + (r % kWpChunks) * 4);
         if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
-            dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
+            dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
     }
 }
 
@@ -651,7 +681,7 @@ __device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, 
     const int e0 = min(lane, kStreamChunks<T> - 1) * E;
     const int i = min(max(t * kW + (e0 >> 3), 0), gm.L - 1);
     if (lane < kStreamChunks<T>)   // the lanes with a chunk only (kTmStageBytes)
-        dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
+        dma16_pol<TD_TDMA_POLICY>(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
 }
 
 // staged tempmax of window t -> its LDS slot (beta input)
@@ -872,7 +902,7 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
             off = ck_step<ALGO>(r) * row_bytes + (w / blk) * blk + pc * 16;
         }
-        if (q + 1 < n || b < alpha_dma_bytes<T, ALGO>()) dma16(lds + q * kDmaBytes, src + off);
+        if (q + 1 < n || b < alpha_dma_bytes<T, ALGO>()) dma16_pol<TD_ADMA_POLICY>(lds + q * kDmaBytes, src + off);
     }
 #endif
 }
