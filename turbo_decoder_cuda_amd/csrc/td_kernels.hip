@@ -597,8 +597,11 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
 }
 
 // dma16 with a cache-policy suffix on the load (TD_ADMA_POLICY: the alpha copies, read once)
+// Measured (config 2, one box, 2 rounds, 15-step windows): nt 16.95 / 16.91 ms, sc0 sc1 nt 16.94 /
+// 16.88, sc1 17.15 / 17.22, against 17.14 / 17.21 without: the copy's lines are read once, and not
+// keeping them in L2 / MALL leaves those to the other streams.  Default sc0 sc1 nt.
 #ifndef TD_ADMA_POLICY
-#define TD_ADMA_POLICY 0   // 0: none, 1: nt, 2: sc1, 3: sc0 sc1 nt
+#define TD_ADMA_POLICY 3   // 0: none, 1: nt, 2: sc1, 3: sc0 sc1 nt
 #endif
 #ifndef TD_TDMA_POLICY
 #define TD_TDMA_POLICY 0   // the same for the tile and tempmax stagings
