@@ -561,8 +561,11 @@ __device__ __forceinline__ void gstore(float* p, float v)
 
 // the same with a wave-uniform base in SGPRs, a per-lane 32-bit byte offset and an immediate (the
 // scheduled alpha windows: no per-step 64-bit address arithmetic)
+// 1 (default since v29): the scheduled alpha / tempmax scratch stores carry nt.  With the alpha copy
+// at sc0 sc1 nt: 16.84 / 16.87 / 17.01 ms without, 16.72 / 16.73 / 16.81 with (one box, 3 rounds; with
+// 12-step windows and plain copies the store bits had measured level).
 #ifndef TD_ASTORE_NT
-#define TD_ASTORE_NT 0   // 1: the scheduled alpha / tempmax scratch stores carry nt
+#define TD_ASTORE_NT 1
 #endif
 template <int IMM>
 __device__ __forceinline__ void gstore_s(double* base, unsigned voff, double v)
