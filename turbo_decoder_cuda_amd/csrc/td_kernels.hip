@@ -609,6 +609,9 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
 #ifndef TD_TDMA_POLICY
 #define TD_TDMA_POLICY 0   // the same for the tile and tempmax stagings
 #endif
+#ifndef TD_TDMA_SPLIT
+#define TD_TDMA_SPLIT 0    // 1: TD_TDMA_POLICY on the stream chunks only, the shared permutation chunks plain
+#endif
 template <int POL>
 __device__ __forceinline__ void dma16_pol(unsigned lds, const void* src)
 {
@@ -675,7 +678,16 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const int* pb = r < kWpChunks ? pperm : gm.pi;
         const char* pw = reinterpret_cast<const char*>(pb + ((tc * kW) & ~3) + (r % kWpChunks) * 4);
         if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
-            dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
+        {
+            if constexpr (TD_TDMA_SPLIT) {
+                if (ch < 3 * nc)
+                    dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ps);
+                else
+                    dma16(base + q * kDmaBytes, pw);
+            } else {
+                dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
+            }
+        }
     }
 }
 
