@@ -42,6 +42,12 @@ FRAME_CASES = [
     (8, 1, 2, 0.5, 41, 2, 4, np.float64),
     (24, 1, 6, 0.5, 42, 2, 4, np.float64),
     (10000, 1, 10, 0.8, 43, 1, 4, np.float32),
+    # round 4: trellis lengths L = K+3 at the 15-step window's edge residues -- L = 0 mod 15 (a full
+    # last window, no partial-window loop: K = 72, 432) and L = 1 mod 15 (a one-step last window:
+    # K = 88) -- with their 36.212 Table 5.1.3-3 parameters
+    (72, 7, 18, 0.5, 44, 3, 4, np.float64),
+    (88, 5, 22, 0.5, 45, 3, 4, np.float64),
+    (432, 47, 72, 0.8, 46, 2, 4, np.float64),
 ]
 
 

@@ -50,8 +50,9 @@ def test_batch_vs_oracle_every_iteration(K, f1, f2, B, ebn0):
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
 
 
-# LTE sizes with their 36.212 Table 5.1.3-3 parameters: 5 to 171 windows of the kernel, every
-# residue of L = K+3 mod the 12-step window that LTE sizes take (3, 7, 11), ragged batches
+# LTE sizes with their 36.212 Table 5.1.3-3 parameters: 4 to 137 windows of the kernel's 15-step
+# windows, L = K+3 mod 15 = 6, 14, 3, 4, 5, 11 (the edge residues have their own test below), ragged
+# batches
 @pytest.mark.parametrize("K,f1,f2", [(48, 7, 12), (56, 19, 42), (120, 103, 90), (136, 9, 34),
                                      (512, 31, 64), (2048, 31, 64)])
 @pytest.mark.parametrize("algo", ["logmap", "maxlog"])
@@ -64,6 +65,71 @@ def test_lte_sizes_vs_oracle(K, f1, f2, algo):
         ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
         assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+
+
+# The 15-step window's edge residues (round 4): L = K+3 = 0 mod 15 -- the last window is full, so
+# the B pass has no partial window (K = 72, 192, 432) -- L = 1 mod 15 -- a one-step last window
+# (K = 88) -- and L = 9, 10 mod 15 (K = 216, 352).  LTE sizes, 36.212 Table 5.1.3-3 parameters.
+WINDOW_EDGE_SIZES = [(72, 7, 18), (88, 5, 22), (192, 23, 48), (216, 11, 36), (352, 21, 44), (432, 47, 72)]
+
+
+@pytest.mark.parametrize("K,f1,f2", WINDOW_EDGE_SIZES)
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_window_edge_residues_vs_oracle(K, f1, f2, algo, precision):
+    """Every iteration's bits and Le against the oracle at the window residues L mod 15 = 0, 1, 9, 10,
+    ragged B = 13 (one padded codeword group).  fp64: bits identical, Le within 1e-9 (the oracle's
+    operation order); fp32: the oracle's fp32 restatement, Max-Log-MAP bits identical and log-MAP
+    bits identical at the last iteration (converged frames at 1.5 dB), Le within 1e-3 relative."""
+    B, iters = 13, 4
+    ebn0 = 0.4 if precision == "f64" else 1.5
+    _, flow = O.synth_batch(K, f1, f2, ebn0, 1300 + K, B)
+    if precision == "f32":
+        flow = flow.astype(np.float32)
+    bits, le = _decode_all(K, f1, f2, iters, flow, algo=algo, precision=precision)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(B):
+        ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
+        if precision == "f64":
+            assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
+            assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+            continue
+        if algo == "maxlog":
+            assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
+        else:
+            assert np.array_equal(bits[b, -1], ob[-1].astype(np.uint8)), f"codeword {b}"
+        tol = 2e-3 if algo == "maxlog" else 1e-3
+        assert np.abs(le[b] - ol).max() <= tol * max(1.0, np.abs(ol).max()), f"codeword {b}"
+
+
+@pytest.mark.parametrize("K,f1,f2", [(9, 2, 3), (10, 3, 10), (20, 3, 10), (117, 2, 39)])
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+def test_four_per_cu_w12_residues(monkeypatch, K, f1, f2, algo):
+    """fp32 at four workgroups per CU runs the 12-step-window build (launch_turbo4_w12): B = 6150
+    (769 groups) at L = K+3 = 0, 1, 11, 0 mod 12 (K = 9, 10, 20, 117; LTE sizes only take 3, 7, 11).
+    Bits and Le equal the two-per-CU 15-step kernel's (TD_OCC3=0) exactly, and a sample of codewords
+    matches the oracle's fp32 restatement (Max-Log-MAP bits identical, log-MAP bits identical at the
+    last iteration on converged frames at 2.5 dB, Le within 1e-3 / 2e-3 relative)."""
+    B, iters = 6150, 3
+    _, flow = O.synth_batch(K, f1, f2, 2.5, 4100 + K, B)
+    flow = flow.astype(np.float32)
+    monkeypatch.setenv("TD_OCC3", "0")
+    bits2, le2 = _decode_all(K, f1, f2, iters, flow, algo=algo, precision="f32")
+    monkeypatch.setenv("TD_OCC3", "1")
+    bits4, le4 = _decode_all(K, f1, f2, iters, flow, algo=algo, precision="f32")
+    fast4 = _decode_bits(K, f1, f2, iters, flow, algo=algo, precision="f32")
+    assert np.array_equal(bits2, bits4)
+    assert np.array_equal(le2.view(np.uint8), le4.view(np.uint8))
+    assert np.array_equal(fast4, bits4)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(0, B, 409):
+        ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
+        if algo == "maxlog":
+            assert np.array_equal(bits4[b], ob.astype(np.uint8)), f"codeword {b}"
+        else:
+            assert np.array_equal(bits4[b, -1], ob[-1].astype(np.uint8)), f"codeword {b}"
+        tol = 2e-3 if algo == "maxlog" else 1e-3
+        assert np.abs(le4[b] - ol).max() <= tol * max(1.0, np.abs(ol).max()), f"codeword {b}"
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -297,7 +363,7 @@ def test_one_handle_two_streams():
 @pytest.mark.parametrize("K,f1,f2", [(1, 1, 2), (5, 1, 10), (16, 1, 4)])
 @pytest.mark.parametrize("algo", ["logmap", "maxlog"])
 def test_tiny_K_vs_oracle(K, f1, f2, algo):
-    """Trellises shorter than one 12-step kernel window (L = 4, 8) and one window and a half
+    """Trellises shorter than one 15-step kernel window (L = 4, 8) and one window and a third
     (L = 19): every iteration's bits equal the oracle's, Le within 1e-9 (the reference's own
     frames at K = 8, 24 and 10000 are in tests/golden and run through test_turbo_vs_reference)."""
     B, iters = 9, 3
