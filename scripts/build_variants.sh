@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build kernel variants for an on-box A/B (scripts/variant_ab.sh): one
 # turbo_decoder_cuda_amd/libvar_<name>.so per "name:flags" word of VARIANTS, e.g.
-#   VARIANTS="a_old:-DTD_SCHED=0 b_new:-DTD_SCHED=1" scripts/build_variants.sh
+#   VARIANTS="a_base: b_diag:-DTD_DIAG=1" scripts/build_variants.sh
 # Flags are comma-separated (-DX=1,-DY=2).  Old libvar_*.so are removed first.
 set -e
 cd "$(dirname "$0")/.."

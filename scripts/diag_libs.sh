@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box job: the per-wave cycle split (diag_stamps.py) of each turbo_decoder_cuda_amd/libdiag_*.so
-# (stamps builds of kernel variants, e.g. -DTD_DIAG_NOFOLD).
+# (stamps builds of kernel variants, e.g. -DTD_DIAG=4 (TD_DIAG bits: td_kernels.hip "diagnostic builds")).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out

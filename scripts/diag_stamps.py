@@ -32,7 +32,7 @@ c.profile(True)
 bits = c.decode(x)
 _, kms, _ = c.kernel_ms()
 NS = 14                 # td_kernels.hip kStampSlots
-NW = slots // NS        # waves per group: 4, or 5 with TD_AREC (R = role 4)
+NW = slots // NS        # waves per group: 4
 s = st.cpu().numpy().reshape(G, NW, NS).astype(np.float64)
 L = K + 3
 steps = 2 * iters * L

@@ -433,11 +433,7 @@ int place_ws(td_handle* h, int G)
     return TD_OK;
 }
 
-int groups_for(int B)
-{
-    const int gw = td::groups_per_wg();
-    return ((B + 8 * gw - 1) / (8 * gw)) * gw;   // groups of 8 codewords, whole workgroups
-}
+int groups_for(int B) { return (B + 7) / 8; }   // groups of 8 codewords, one workgroup each
 
 // the windowed schedule's buffers: the workspace's extrinsic pair plus a second pair (concurrent
 // schedule), the alpha checkpoints of each decoder and the NII metrics [2 parity][2 dec][B][nS][2][8],

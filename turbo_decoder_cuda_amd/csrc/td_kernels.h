@@ -30,51 +30,21 @@ bool build_lane_tables(const Trellis& t, LaneTables& lt);
 // Kernel parameter block (passed by value).  Device arrays are batch-interleaved:
 // group g = codewords 8g..8g+7, element [g][step][c].
 constexpr int kPermPad = 32;         // spare ints after pi / pinv: the loader stages window-sized chunks
-// TD_AREC: alpha recomputed in the B pass by a fifth wave per codeword group (td_kernels.hip)
-#ifndef TD_AREC
-#define TD_AREC 0
-#endif
-constexpr int kGroupWaves = TD_AREC ? 5 : 4;   // waves per codeword group (stamp slots per group)
-constexpr int kCuSlotKeys = 2048;   // (XCC, SE, SH, CU) keys of HW_ID
-// alpha scratch (astore) of one codeword group: L rows of 64 (8 codewords x 8 states) plus a pad of
-// TD_APAD elements between the groups' streams (a knob: pads of 512 B, 4 KiB and 32.5 KiB left the
-// placement modes of DESIGN.md 3.2 as they were)
-#ifndef TD_APAD
-#define TD_APAD 0
-#endif
-constexpr size_t astore_group_elems(int L) { return (size_t)L * 64 + TD_APAD; }
-// Alpha scratch layout (TD_AWIN, a knob): 0 (default) group-major [G][L][64] (+ TD_APAD per
-// group); 1 window-major [nT][G][kWindowSteps][64] (window t of every group one contiguous region);
-// 2 step-major [nT * kWindowSteps][G][64] (the row of step i of every group one 32 KiB span).
-// Measured in round 3 against the placement modes of DESIGN.md 3.2: all three keep the two modes
-// (fast 17.6-17.9 ms / slow 18.5-19.2 ms at config 2, plain allocations), and group-major has the
-// fastest fast mode, so it stays the default; td_reserve's placement search remains the remedy.
-#ifndef TD_AWIN
-#define TD_AWIN 0
-#endif
+constexpr int kGroupWaves = 4;       // waves per codeword group (stamp slots per group)
+constexpr int kCuSlotKeys = 2048;    // (XCC, SE, SH, CU) keys of HW_ID
 // Trellis steps per window of the exact schedule (td_kernels.hip kW): a multiple of 3 (the label
-// period) with at most 128 (step, codeword) fold items (two fold waves, one item per lane), so 12 or 15.
-#ifndef TD_KW
-#define TD_KW 15
-#endif
-constexpr int kWindowSteps = TD_KW;   // td_kernels.hip kW
-constexpr int awin_windows(int L) { return (L + kWindowSteps - 1) / kWindowSteps; }
-constexpr size_t astore_elems(int G, int L)
-{
-    return TD_AWIN ? (size_t)awin_windows(L) * G * kWindowSteps * 64
-                   : (size_t)G * astore_group_elems(L) + (size_t)kWindowSteps * 64;   // + one window: DMA tail
-}
-// element offset of row 0 of window t of group g
-constexpr size_t astore_window_off(int g, int t, int G, int L)
-{
-    return TD_AWIN == 2 ? ((size_t)t * kWindowSteps * G + g) * 64
-         : TD_AWIN      ? ((size_t)t * G + g) * kWindowSteps * 64
-                        : (size_t)g * astore_group_elems(L) + (size_t)t * kWindowSteps * 64;
-}
-// distance between the first rows of windows t and t+1 of one group
-constexpr size_t astore_window_stride(int G) { return TD_AWIN ? (size_t)G * kWindowSteps * 64 : (size_t)kWindowSteps * 64; }
-// distance between consecutive rows (steps) of one group
-constexpr size_t astore_row_stride(int G) { return TD_AWIN == 2 ? (size_t)G * 64 : 64; }
+// period) with at most 128 (step, codeword) fold items (two fold waves, one item per lane), so 12 or
+// 15.  The library builds 15 (td_kernels.hip) and 12 (td_kernels_w12.hip, fp32 at four per CU); the
+// host sizes every buffer for the larger and reads the decode's own window count from
+// td::window_steps().
+constexpr int kWindowStepsMax = 15;
+// Alpha scratch (astore): group-major [G][L][64] (8 codewords x 8 states per step and group), plus
+// one window of the longest window length after the last group: the loader copies whole windows, so
+// the last group's last window reads past its L rows.  (Window-major and step-major layouts and pads
+// between the groups' streams were measured in round 3: none removed the placement modes of DESIGN.md
+// 3.2, and group-major had the fastest fast mode.)
+constexpr size_t astore_group_elems(int L) { return (size_t)L * 64; }
+constexpr size_t astore_elems(int G, int L) { return (size_t)G * astore_group_elems(L) + (size_t)kWindowStepsMax * 64; }
 
 template <typename T>
 struct DecodeParams {
@@ -84,7 +54,7 @@ struct DecodeParams {
     T* par2;   // [G][L][8] parity 2
     T* ext12;  // [G][K][8] Le of decoder 1 scattered to interleaved order (= La of decoder 2)
     T* ext21;  // [G][K][8] Le of decoder 2 scattered to natural order (= La of decoder 1)
-    T* astore;    // alpha[.][i] by 8c + state (F pass -> B pass scratch), windows at astore_window_off
+    T* astore;    // alpha[.][i] by 8c + state (F pass -> B pass scratch), [G][L][64] (astore_elems)
     T* tmstore;   // [G][L][8] tempmax[i+1] per step and codeword
     T* llr_out;                 // bare SISO: [G][L][8]
     const int* pi;              // [K] QPP
@@ -160,7 +130,6 @@ hipError_t launch_demodulate(const double* yi, const double* yq, long long nsym,
 hipError_t launch_count_errors(const uint8_t* bits, const uint8_t* info, int K, int iters, int B, int* err,
                                hipStream_t st);
 
-int window_steps();
-int groups_per_wg();   // codeword groups (of 8) per workgroup: G must be a multiple of this
+int window_steps();   // steps per window of the exact schedule's two-per-CU kernel (td_kernels.hip kW)
 
 }  // namespace td

@@ -14,7 +14,7 @@
 // alpha/beta critical path except the max* table (one ds_read per max*).
 //
 // SISO = Log_MAP_decoder (ITTC/log_map.cpp:898-1047) in the serial schedule of TurboDecoding
-// (:1217-1265).  Per SISO, over windows of kW = 12 trellis steps:
+// (:1217-1265).  Per SISO, over windows of kW = 15 trellis steps (12 in the td_kernels_w12.hip build):
 //   F pass  wave A runs alpha forward over the L = K+3 steps and streams alpha of EVERY step (by
 //           state, 512 B per group and step in fp64) and the reference's tempmax (:986-993) to an
 //           HBM scratch (astore / tmstore); Max-Log-MAP stores alpha one step in three and the
@@ -45,27 +45,40 @@ using namespace ::td;
 namespace td {
 #endif
 
-constexpr int kW = kWindowSteps;                // steps per window (multiple of 3; td_kernels.h TD_KW)
+#ifndef TD_KW
+#define TD_KW 15   // td_kernels_w12.hip: 12
+#endif
+constexpr int kW = TD_KW;                       // steps per window (multiple of 3; td_kernels.h kWindowStepsMax)
 static_assert(kW == 12 || kW == 15, "windows of 12 or 15 steps");
+static_assert(kW <= kWindowStepsMax, "the host sizes the alpha scratch's DMA tail for the longest window");
 constexpr int kArow0 = kW / 2;                  // scheduled alpha stores: rows addressed from row kArow0 (immediates)
 constexpr int kCw = 8;                          // codewords per workgroup
 constexpr int kLanes = 64;
 constexpr int kTile = kW * kCw;                 // (step, codeword) elements per window
 static_assert(kW % 3 == 0, "window must be a multiple of the label period");
 
+// ------------------------------------------------------------------ diagnostic builds
+// TD_DIAG, a bit mask (0, the product, unless a diagnostic library is built with -DTD_DIAG=n):
+// timing-only builds whose decoded results are WRONG, used to attribute the kernel's time
+// (DESIGN.md 3.2).  No test, smoke() or bench.py run loads them.
+#ifndef TD_DIAG
+#define TD_DIAG 0
+#endif
+constexpr unsigned kDiagNoAdma = 1;       // the B pass without the loader's alpha copies
+constexpr unsigned kDiagNoBConvert = 2;   // the B pass without the loader's tile / tempmax converts
+constexpr unsigned kDiagNoFold = 4;       // the B pass without its folds
+constexpr unsigned kDiagNoBeta = 8;       // the B pass without the beta chain
+template <unsigned D>
+constexpr bool kDiag = (TD_DIAG & D) != 0;
+
 // Alpha rows kept in the F pass -> B pass scratch, by phase i mod 3 (bit p: steps i = p mod 3).
-#ifndef TD_CK_PHASES
-#define TD_CK_PHASES 1   // bit p: alpha of the steps i = p mod 3 is stored (max-log)
-#endif
-// Log-MAP may store a subset of the rows as well (TD_CK_PHASES_LOGMAP; 7 = every row, the
-// default): the folds then recompute the missing rows with the table max*, bit-identical to the
-// alpha wave (alpha_recompute), in exchange for less scratch traffic.
-#ifndef TD_CK_PHASES_LOGMAP
-#define TD_CK_PHASES_LOGMAP 7
-#endif
-constexpr int kCkPhases = TD_CK_PHASES | 1;
+// Log-MAP keeps every row; Max-Log-MAP only the rows of phase 0, and its folds recompute the two
+// steps in between (alpha_recompute).  Log-MAP keeping a subset measured 16 % (phases {0, 1}) and 40 %
+// (phase 0) slower in round 3: eight table max* per recomputed step cost the fold waves more than
+// the scratch traffic costs the kernel; Max-Log-MAP keeping two phases in three
+// measured slower than one (1635 vs 1860 Mbit/s).
 template <int ALGO>
-constexpr int kCkPh = ALGO == 1 ? kCkPhases : (TD_CK_PHASES_LOGMAP | 1);   // stored phases of this algorithm
+constexpr int kCkPh = ALGO == 1 ? 1 : 7;                                      // stored phases of this algorithm
 template <int ALGO>
 constexpr bool kCkAll = kCkPh<ALGO> == 7;                                    // every row stored
 // the phase whose steps sit furthest from a kept row (recomputed through the most steps)
@@ -120,32 +133,17 @@ __device__ __forceinline__ T group_max8(T v)
     return v;
 }
 
-// The alpha step's tempmax (the max over the codeword's 8 lanes) and the partner's metric an.
-// TD_QMAX=1: the three quad mates are read in one DPP level (quad_perm xor 1, 2, 3), their max is
-// a two-deep tree, and one row_half_mirror of it brings the other quad's: DPP, max, max, DPP, max
-// on the chain instead of three (DPP, max) levels, for two more VALU ops (and, at phase 2, the
-// partner's mirror beside the tree).  Exact in any order.  Measured slower on one box (2 interleaved
-// rounds, B=4096): fp64 log-MAP 17.51 -> 17.80 ms, fp64 max-log 11.56 -> 11.74, fp32 max-log 10.36 ->
-// 10.56; fp32 log-MAP 15.17 -> 15.10.  In fp64 the DPP pairs' issue, not their hazard, is the cost,
-// and the tree issues the same movs ahead of its first max.  Default off.
-#ifndef TD_QMAX
-#define TD_QMAX 0
-#endif
-constexpr int kDppXor3 = 0x1B;    // quad_perm [3,2,1,0]
+// The alpha step's tempmax (the max over the codeword's 8 lanes) and the partner's metric an: three
+// (DPP, max) levels, the first one the partner exchange of this phase.  (A quad tree -- the three
+// quad mates in one DPP level, then one row_half_mirror -- measured 0.4-1.7 % slower in round 3: in
+// fp64 the DPP pairs' issue, not their hazard, is the cost.)
 template <typename T, int PH>
 __device__ __forceinline__ T alpha_tempmax(T a, T& an)
 {
-    if constexpr (TD_QMAX != 0) {
-        const T x1 = dpp<kDppXor1>(a), x2 = dpp<kDppXor2>(a), x3 = dpp<kDppXor3>(a);
-        const T q = vmax(vmax(a, x1), vmax(x2, x3));
-        an = PH == 0 ? x1 : (PH == 1 ? x2 : dpp<kDppMir8>(a));
-        return vmax(q, dpp<kDppMir8>(q));
-    } else {
-        an = dpp<PhaseDpp<PH>::ctrl>(a);
-        T m = vmax(a, an);
-        m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
-        return vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
-    }
+    an = dpp<PhaseDpp<PH>::ctrl>(a);
+    T m = vmax(a, an);
+    m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+    return vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
 }
 
 // ------------------------------------------------------------------ max*
@@ -180,25 +178,10 @@ constexpr int kLutRows = kLutSize + 1;   // + a pad row: v[q+1] for the last buc
 // fp32: 32 columns.  Its 4-byte reads are served 32 lanes per LDS cycle on 32 banks, so with 16
 // columns lanes l and l+16 shared a bank whenever their buckets differed (SQ_LDS_BANK_CONFLICT
 // was 28 % of the fp32 kernel's LDS cycles).  fp64 keeps 16: 8-byte elements in 16 columns
-// already cover the 32 banks that ds_read2_b64 serves per cycle, and 32 would not fit in LDS.
-#ifndef TD_LUT32
-#define TD_LUT32 1
-#endif
-#ifndef TD_LUT32_F64
-#define TD_LUT32_F64 0   // fp64 table in 32 columns (fits since the table went to 29 buckets)
-#endif
-// TD_LUT_SPLIT (fp64): a row's three fields as three ds_read_b64 (2 LDS cycles each, 32 lanes per
-// cycle, conflict-free on the 32-column table) instead of ds_read2_b64 + ds_read_b64 (8 + 2 cycles:
-// ds_read2_b64 serves 16 lanes per cycle, MI355X_MICROARCH.md LDS table).  The B pass keeps the LDS
-// array busy ~70 % of its time (SQ_LDS_IDX_ACTIVE), so LDS cycles are latency for the fold chains.
-// 1: every table read; 2: the folds' (mstar / lut_pick) only.  Forces the 32-column fp64 table.
-// Measured slower (one box, 3 rounds, config 2): 17.53 ms base, 17.85 with 1, 18.50 with 2 (the
-// volatile reads also fix the fold chains' read order); default off.
-#ifndef TD_LUT_SPLIT
-#define TD_LUT_SPLIT 0
-#endif
+// already cover the 32 banks that ds_read2_b64 serves per cycle (32 columns measured level, and a
+// row read as three ds_read_b64 from them 2-6 % slower: DESIGN.md 3.2).
 template <typename T>
-constexpr int kLutCols = (TD_LUT32 && sizeof(T) == 4) || ((TD_LUT32_F64 || TD_LUT_SPLIT) && sizeof(T) == 8) ? 32 : 16;
+constexpr int kLutCols = sizeof(T) == 4 ? 32 : 16;
 template <typename T>
 constexpr int kLutElems = 2 * kLutRows * kLutCols<T>;
 
@@ -225,28 +208,19 @@ __device__ __forceinline__ LutRow lut_row(T d)
 {
     return LutRow{bucket_dev<T>(d) * 2 * kLutCols<T>};
 }
-// the row's threshold and its two values (FOLD: a fold / recompute read, see TD_LUT_SPLIT); volatile
-// keeps the three reads from being merged into a ds_read2_b64
-template <typename T, bool FOLD = false>
+// the row's threshold and its two values
+template <typename T>
 __device__ __forceinline__ void lut_fields(const T* lut, int o, T& thr, T& lo, T& hi)
 {
-    if constexpr (sizeof(T) == 8 && (TD_LUT_SPLIT == 1 || (TD_LUT_SPLIT == 2 && FOLD))) {
-        typedef __attribute__((address_space(3))) const volatile T lds_t;
-        lds_t* v = (lds_t*)lut;
-        thr = v[o];
-        lo = v[o + kLutCols<T>];
-        hi = v[o + 3 * kLutCols<T>];
-    } else {
-        thr = lut[o];
-        lo = lut[o + kLutCols<T>];
-        hi = lut[o + 3 * kLutCols<T>];
-    }
+    thr = lut[o];
+    lo = lut[o + kLutCols<T>];
+    hi = lut[o + 3 * kLutCols<T>];
 }
 template <typename T>
 __device__ __forceinline__ T lut_pick(const T* lut, LutRow r, T d)
 {
     T thr, lo, hi;
-    lut_fields<T, true>(lut, r.o, thr, lo, hi);
+    lut_fields<T>(lut, r.o, thr, lo, hi);
     return fabs(d) >= thr ? hi : lo;
 }
 
@@ -317,63 +291,16 @@ __device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneC
 //                         codeword) item per lane, both input bits in the same lane.
 // Only the two recursions are serial chains; nothing else waits on them but the barriers.  The
 // barriers are raw `s_waitcnt lgkmcnt(0); s_barrier`, so prefetched global loads stay in flight.
-// TD_AREC (td_kernels.h): the F pass streams only one alpha row per window (alpha_raw entering the
-// window's first step, the checkpoint) and a fifth wave R recomputes alpha over each window in the B
-// pass, beside beta, into an LDS ring the folds read -- the alpha scratch stream (63 % of the HBM
-// traffic) shrinks twelvefold, and the Av ring to two windows, so that three workgroups fit a CU.
-constexpr bool kArec = TD_AREC != 0;
-constexpr int kWaves = kGroupWaves;                  // waves per codeword group (5 with TD_AREC)
-#ifndef TD_GROUPS_PER_WG
-#define TD_GROUPS_PER_WG 1
-#endif
-#ifndef TD_ROLE_XOR
-#define TD_ROLE_XOR 1
-#endif
-// Codeword groups per workgroup.  With two, the groups run in lock step (shared barriers) and the
-// second group permutes its roles (role = (wave & 3) ^ TD_ROLE_XOR) so that waves w and w+4, which
-// share a SIMD, never hold the same role: the two alpha chains of the forward pass get a SIMD each.
-constexpr int kGroupsPerWg = TD_GROUPS_PER_WG;
-constexpr int kFoldPerWave = kTile / 2;              // items per folding wave (A and F1) per window
-static_assert(kFoldPerWave <= kLanes, "one fold item per lane");
-// log-MAP: fold items of wave A (its SIMD partner is the other workgroup's loader) per window; F1,
-// which shares its SIMD with the other workgroup's beta, takes the remaining kTile - kFoldA
-#ifndef TD_FOLD_A
-#define TD_FOLD_A (kTile / 2)
-#endif
-// TD_FOLD_SPLIT (log-MAP): wave A folds 64 items (both E_seq chains in each lane) and F1 -- the
-// B pass's slowest wave (stamps: 195 cycles a step against 171-176 for the others), because it
-// shares its SIMD with the other workgroup's beta -- folds the other 32 with one chain per lane
-// (temp0 in lanes 0-31, temp1 in lanes 32-63), half the instructions of a two-chain item, and
-// the two halves meet through one lane exchange (fold_item_split).  Parity-green, measured level
-// (18.69-18.77 ms against 18.69-18.77, one box, 3 rounds): F1's instruction count does not set the
-// B pass.  Default off.
-#ifndef TD_FOLD_SPLIT
-#define TD_FOLD_SPLIT 0
-#endif
-template <int ALGO>
-constexpr bool kFoldSplit = TD_FOLD_SPLIT != 0 && ALGO == 0;
-template <int ALGO>
-constexpr int kFoldA = ALGO == 0 ? (kFoldSplit<ALGO> ? kLanes : TD_FOLD_A) : kFoldPerWave;
-#ifndef TD_ML_FOLD_MAP
-#define TD_ML_FOLD_MAP 1   // Max-Log-MAP fold items split by recompute depth (siso_wg B pass)
-#endif
-static_assert(TD_FOLD_A <= kLanes && kTile - TD_FOLD_A <= kLanes, "one fold item per lane");
-constexpr int kAvSlots = kArec ? 2 : 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3);
-                                          // TD_AREC: written by R one iteration before its fold
-// TD_AV_DIRECT: the fold lanes load their alpha blocks (8 states, 64 B in fp64) from the HBM scratch
-// into registers one window ahead, instead of the loader copying whole windows into an LDS ring
-// (Av): the ring is 24.6 KB of the fp64 workgroup's 69.9 KB of LDS, without it three workgroups fit
-// a CU (turbo_decode_kernel3).  Same bytes from HBM; no alpha LDS writes or reads.
-#ifndef TD_AV_DIRECT
-#define TD_AV_DIRECT 0
-#endif
-constexpr bool kAvDirect = TD_AV_DIRECT != 0;
-static_assert(!(kAvDirect && kArec), "TD_AV_DIRECT and TD_AREC exclude each other");
-static_assert(!(TD_FOLD_SPLIT && (kAvDirect || kArec || TD_CK_PHASES_LOGMAP != 7)),
-              "TD_FOLD_SPLIT folds from the alpha ring with every row kept");
+// (Measured and retired in round 3, numbers in DESIGN.md 3.2 / 6: a fifth wave recomputing alpha in
+// the B pass from one checkpoint per window, -10 % at B = 4096; the fold lanes loading their alpha
+// blocks from HBM instead of the Av ring, -9 %; F1 folding with one E_seq chain per lane, level.)
+constexpr int kWaves = kGroupWaves;                  // waves per codeword group
+constexpr int kFoldA = kTile / 2;                    // items per folding wave (A and F1) per window
+static_assert(kFoldA <= kLanes, "one fold item per lane");
+constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 // every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
 template <int ALGO>
-constexpr bool kFoldRows = kArec || kCkAll<ALGO>;
+constexpr bool kFoldRows = kCkAll<ALGO>;
 
 // Loader staging.  Window inputs travel HBM -> LDS by DMA (global_load_lds_dwordx4: no VGPR
 // destination, completion counted by vmcnt; LDS target = wave-uniform base + 16 * lane) and the
@@ -404,8 +331,7 @@ struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     int Wp[3][kW][2];          // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
-    alignas(16) T Av[kAvDirect ? 1 : kAvSlots][kAvDirect ? 1 : kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state
-                                                                    // (fold input, DMA from HBM; unused: TD_AV_DIRECT)
+    alignas(16) T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
     alignas(16) unsigned char stage[3][kStageBytes<T>];     // loader: staged window inputs
@@ -422,11 +348,8 @@ struct Smem {
 // per-lane source addresses (the DMA's LDS side stays linear); beta publishes to rotated offsets.
 // A/B on one box: fp64 log-MAP 1180 -> 1211 Mbit/s, fp64 max-log 1900 -> 1928; fp32 lost 2 %
 // (1403 -> 1378, 2389 -> 2344), so fp32 keeps plain blocks.
-#ifndef TD_FOLD_SWZ
-#define TD_FOLD_SWZ 1   // 0: plain blocks, 1: rotated in fp64, 2: rotated in both precisions
-#endif
 template <typename T>
-constexpr bool kFoldSwz = TD_FOLD_SWZ == 2 || (TD_FOLD_SWZ == 1 && sizeof(T) == 8);
+constexpr bool kFoldSwz = sizeof(T) == 8;
 template <typename T>
 constexpr int kBlkChunks = 8 * (int)sizeof(T) / 16;   // 16-B chunks per (row, codeword) block
 // element offset of state s (0..7) inside the block of row r
@@ -456,14 +379,11 @@ __device__ __forceinline__ void load_block(const T* blk, int r, T (&v)[8])
 }
 // Rotation of alpha block (row r, codeword c).  Log-MAP: r (rows are the fold lanes' steps k).
 // Max-Log-MAP rows are checkpoints, r = k / 3, so the read groups hold up to three lanes of one
-// row; rotating by r + 2 (c >> 2) keeps their blocks' slots apart as well.
-#ifndef TD_MLAV_ROT
-#define TD_MLAV_ROT 1
-#endif
+// row; rotating by r + 2 (c >> 2) keeps their blocks' slots apart as well (+0.6 %, config 3).
 template <int ALGO>
 __device__ __forceinline__ int av_rot(int r, int c)
 {
-    return (!kCkAll<ALGO> && TD_MLAV_ROT) ? r + 2 * (c >> 2) : r;
+    return !kCkAll<ALGO> ? r + 2 * (c >> 2) : r;
 }
 // row offset 8c + s (st_off) -> rotated
 template <typename T>
@@ -560,20 +480,13 @@ __device__ __forceinline__ void gstore(float* p, float v)
 }
 
 // the same with a wave-uniform base in SGPRs, a per-lane 32-bit byte offset and an immediate (the
-// scheduled alpha windows: no per-step 64-bit address arithmetic)
-// 1 (default since v29): the scheduled alpha / tempmax scratch stores carry nt.  With the alpha copy
-// at sc0 sc1 nt: 16.84 / 16.87 / 17.01 ms without, 16.72 / 16.73 / 16.81 with (one box, 3 rounds; with
-// 12-step windows and plain copies the store bits had measured level).
-#ifndef TD_ASTORE_NT
-#define TD_ASTORE_NT 1
-#endif
+// scheduled alpha windows: no per-step 64-bit address arithmetic).  The fp64 stores carry nt (v29:
+// with the alpha copy at sc0 sc1 nt, 16.84 / 16.87 / 17.01 ms without, 16.72 / 16.73 / 16.81 with; one
+// box, 3 rounds); the fp32 stores are plain (never measured with nt).
 template <int IMM>
 __device__ __forceinline__ void gstore_s(double* base, unsigned voff, double v)
 {
-    if constexpr (TD_ASTORE_NT)
-        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
-    else
-        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
+    asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v), "s"(base), "n"(IMM) : "memory");
 }
 template <int IMM>
 __device__ __forceinline__ void gstore_s(float* base, unsigned voff, float v)
@@ -599,50 +512,15 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
                  : "memory");
 }
 
-// dma16 with a cache-policy suffix on the load (TD_ADMA_POLICY: the alpha copies, read once)
-// Measured (config 2, one box, 2 rounds, 15-step windows): nt 16.95 / 16.91 ms, sc0 sc1 nt 16.94 /
-// 16.88, sc1 17.15 / 17.22, against 17.14 / 17.21 without: the copy's lines are read once, and not
-// keeping them in L2 / MALL leaves those to the other streams.  Default sc0 sc1 nt.
-#ifndef TD_ADMA_POLICY
-#define TD_ADMA_POLICY 3   // 0: none, 1: nt, 2: sc1, 3: sc0 sc1 nt
-#endif
-#ifndef TD_TDMA_POLICY
-#define TD_TDMA_POLICY 0   // the same for the tile and tempmax stagings
-#endif
-#ifndef TD_TDMA_SPLIT
-#define TD_TDMA_SPLIT 0    // 1: TD_TDMA_POLICY on the stream chunks only, the shared permutation chunks plain
-#endif
-template <int POL>
-__device__ __forceinline__ void dma16_pol(unsigned lds, const void* src)
+// dma16 with sc0 sc1 nt on the load: the alpha copies, whose lines are read once -- not keeping them
+// in L2 / MALL leaves those to the other streams.  Measured (config 2, one box, 2 rounds): nt 16.95 /
+// 16.91 ms, sc0 sc1 nt 16.94 / 16.88, sc1 17.15 / 17.22, against 17.14 / 17.21 without.  The same bits
+// on the tile stagings (read twice) measured level or slower, so those stay plain.
+__device__ __forceinline__ void dma16_stream(unsigned lds, const void* src)
 {
     unsigned save;
-    if constexpr (POL == 1)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
-    else if constexpr (POL == 2)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off sc1\n\ts_mov_b32 m0, %0"
-                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
-    else if constexpr (POL == 3)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off sc0 sc1 nt\n\ts_mov_b32 m0, %0"
-                     : "=&s"(save) : "s"(lds), "v"(src) : "memory");
-    else
-        dma16(lds, src);
-}
-
-// dma16 with a wave-uniform SGPR base and a per-lane 32-bit byte offset (saddr form)
-// alpha_dma through dma16_s: 17 VGPRs fewer in the fp64 log-MAP kernel (256 -> 239), but 0.9 %
-// slower on one box (17.47 vs 17.31 ms, 3 interleaved rounds), so the per-lane 64-bit form stays the
-// default; the step-major alpha layout (TD_AWIN 2) needs the saddr form.
-#ifndef TD_ADMA_SADDR
-#define TD_ADMA_SADDR (TD_AWIN == 2)
-#endif
-__device__ __forceinline__ void dma16_s(unsigned lds, const void* sbase, unsigned voff)
-{
-    unsigned save;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
-                 : "=&s"(save)
-                 : "s"(lds), "v"(voff), "s"(sbase)
-                 : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off sc0 sc1 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save) : "s"(lds), "v"(src) : "memory");
 }
 
 // Stage window t (rows clamped into range, so the count of DMA instructions never varies; values
@@ -678,16 +556,7 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const int* pb = r < kWpChunks ? pperm : gm.pi;
         const char* pw = reinterpret_cast<const char*>(pb + ((tc * kW) & ~3) + (r % kWpChunks) * 4);
         if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
-        {
-            if constexpr (TD_TDMA_SPLIT) {
-                if (ch < 3 * nc)
-                    dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ps);
-                else
-                    dma16(base + q * kDmaBytes, pw);
-            } else {
-                dma16_pol<TD_TDMA_POLICY>(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
-            }
-        }
+            dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
     }
 }
 
@@ -699,7 +568,7 @@ __device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, 
     const int e0 = min(lane, kStreamChunks<T> - 1) * E;
     const int i = min(max(t * kW + (e0 >> 3), 0), gm.L - 1);
     if (lane < kStreamChunks<T>)   // the lanes with a chunk only (kTmStageBytes)
-        dma16_pol<TD_TDMA_POLICY>(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
+        dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
 }
 
 // staged tempmax of window t -> its LDS slot (beta input)
@@ -747,93 +616,23 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
 
-// tile_convert (TILE) and tm_convert (TM) of one B-pass iteration with every LDS read issued before
-// the first write: written as two functions, each pass's reads waited for the previous pass's
-// writes (the compiler cannot tell the staging slots from the rings), four dependent LDS round trips
-// per window -- ~108 cycles a step of the loader's ~170, which sets the B pass with 15-step windows.
-#ifndef TD_CONVERT_BATCH
-#define TD_CONVERT_BATCH 0   // measured level (17.20-17.26 vs 17.25-17.28 ms, one box, 3 rounds): off
-#endif
-template <typename T>
-__device__ __forceinline__ void bpass_convert(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int lane, bool tile,
-                                              bool tm)
-{
-    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
-    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);
-    const T* sv = reinterpret_cast<const T*>(&sm.tmstage[slot][0]);
-    T ys[2], yp[2], la[2], tv[2];
-    int w0 = 0, w1 = 0;
-    const int k0 = lane >> 3;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = min(lane + kLanes * q, kTile - 1);
-        if (tile) {
-            ys[q] = sy[e];
-            yp[q] = sy[kTile + e];
-            la[q] = sy[2 * kTile + e];
-        }
-        if (tm) tv[q] = sv[e];
-    }
-    if (tile && (lane & 7) == 0) {
-        w0 = sw[min(k0, kW - 1)];
-        w1 = sw[kWpInts + min(k0, kW - 1)];
-    }
-    int w0b = 0, w1b = 0;
-    if (tile && (lane & 7) == 0 && k0 + 8 < kW) {
-        w0b = sw[k0 + 8];
-        w1b = sw[kWpInts + k0 + 8];
-    }
-    __builtin_amdgcn_sched_barrier(0);   // every read above is in flight before any write below
-    if (tile) {
-        T* g = &sm.G[t % 3][0][0][0];
-        int* w = &sm.Wp[t % 3][0][0];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int e = lane + kLanes * q;
-            if (e < kTile) {
-                const int k = e >> 3;
-                const T l = la_at(src, t * kW + k, la[q]);
-                const T hla = l / (T)2;
-                g[4 * e] = (ys[q] + yp[q]) + hla;
-                g[4 * e + 1] = (ys[q] - yp[q]) + hla;
-                g[4 * e + 2] = ys[q];
-                g[4 * e + 3] = l;
-            }
-        }
-        if ((lane & 7) == 0) {   // one entry per step: every codeword has the same positions
-            if (k0 < kW) {
-                w[2 * k0] = w0;
-                w[2 * k0 + 1] = w1;
-            }
-            if (k0 + 8 < kW) {
-                w[2 * (k0 + 8)] = w0b;
-                w[2 * (k0 + 8) + 1] = w1b;
-            }
-        }
-    }
-    if (tm) {
-        T* d = &sm.tm[t & 1][0][0];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int e = lane + kLanes * q;
-            if (e < kTile) d[e] = tv[q];
-        }
-    }
-}
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
 
-// ---- alpha / tempmax of a window, HBM scratch -> registers -> LDS (wave F0, B pass).
-// Scratch layout: alpha by 8c + state in windows of kW rows (astore_window_off: window-major
-// [nT][G][kW][64] by default, td_kernels.h TD_AWIN), tempmax [g][L][8].
-// alpha of window t: HBM scratch -> LDS slot t % 3 directly (global_load_lds_dwordx4, no
-// registers): the window's kW rows are one contiguous 6 KiB block on both sides.  Completion is
-// tracked by vmcnt; the loader waits for it before the barrier that publishes the slot.
-// Max-Log-MAP stores alpha only at the steps of the phases in kCkPhases (i mod 3; phase 0 always)
-// and the folds recompute the steps in between from the last stored one (alpha_recompute): less
-// alpha traffic, which otherwise bounds its forward pass (HBM writes).  The copy gathers the
-// window's stored rows into consecutive LDS rows.
-// (TD_CK_PHASES / TD_CK_PHASES_LOGMAP, kCkPh, kCkAll: see the top of the file)
+// ---- alpha of a window, HBM scratch -> LDS (wave F0, B pass).
+// Scratch layout: alpha by 8c + state, group-major [G][L][64] (td_kernels.h astore_elems), tempmax
+// [g][L][8].
+// alpha of window t: HBM scratch -> LDS slot t % 4 directly (global_load_lds_dwordx4, no
+// registers): the window's kW rows are one contiguous block on both sides.  Completion is tracked
+// by vmcnt; the loader waits for it before the barrier that publishes the slot.
+// Max-Log-MAP stores alpha only at the steps of phase 0 (kCkPh) and the folds recompute the steps in
+// between from the last stored one (alpha_recompute): less alpha traffic, which otherwise bounds its
+// forward pass (HBM writes).  The copy gathers the window's stored rows into consecutive LDS rows.
+// element offset of row 0 of window t of group g in the alpha scratch
+__device__ __forceinline__ size_t astore_window_off(int g, int t, int L)
+{
+    return (size_t)g * astore_group_elems(L) + (size_t)t * kW * 64;
+}
 template <int ALGO>
 constexpr int kCkPerGroup = (kCkPh<ALGO> & 1) + ((kCkPh<ALGO> >> 1) & 1) + ((kCkPh<ALGO> >> 2) & 1);
 template <int ALGO>
@@ -863,7 +662,7 @@ __device__ __forceinline__ int ck_row_of(int k, int& ks)
 template <typename T, int ALGO>
 constexpr int alpha_dma_count()
 {
-    return (kAvDirect || kArec) ? 0 : (kCkRows<ALGO> * kLanes * (int)sizeof(T) + kDmaBytes - 1) / kDmaBytes;
+    return (kCkRows<ALGO> * kLanes * (int)sizeof(T) + kDmaBytes - 1) / kDmaBytes;
 }
 // bytes of a window's stored alpha rows (the last DMA covers the lanes below it only)
 template <typename T, int ALGO>
@@ -873,43 +672,19 @@ constexpr int alpha_dma_bytes()
 }
 static_assert(kW % 3 == 0, "stored rows repeat every 3 window-relative steps");
 
+// A 64-bit per-lane source pointer per DMA.  (The saddr form -- an SGPR base and 32-bit per-lane
+// offsets -- saves 17 VGPRs but measured 0.9 % slower, round 3.)  LDS row r holds the window's step r
+// (max-log: ck_step(r)); chunk pc of codeword block cb holds the block's chunk (pc - av_rot) mod
+// kBlkChunks (blk_off).
 template <typename T, int ALGO>
 __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Geom& gm, int t, int lane)
 {
     const int slot = ((t % kAvSlots) + kAvSlots) % kAvSlots;
     const int tc = max(t, 0);
-#ifdef TD_DIAG_ADMA_L2   // diagnostics only (wrong results): every copy reads window 0 of group 0 (L2-resident)
-    const char* src = reinterpret_cast<const char*>(astore);
-#else
-    const char* src = reinterpret_cast<const char*>(astore + astore_window_off(gm.g, tc, gm.G, gm.L));
-#endif
+    const char* src = reinterpret_cast<const char*>(astore + astore_window_off(gm.g, tc, gm.L));
     const unsigned lds = lds_addr(&sm.Av[slot][0][0]);
     constexpr int n = alpha_dma_count<T, ALGO>();
     constexpr int row_bytes = kLanes * (int)sizeof(T);   // one step of the window
-    // saddr form (TD_ADMA_SADDR): the window's rows are arow_bytes apart (step-major: G groups;
-    // else contiguous).  Each DMA covers rpd LDS rows; its first source row is a wave-uniform SGPR
-    // base, the lane's row and chunk within it a 32-bit offset.  LDS row r holds the window's step
-    // r (max-log: ck_step(r)); chunk pc of codeword block cb holds the block's chunk
-    // (pc - av_rot) mod kBlkChunks (blk_off).
-#if TD_ADMA_SADDR
-    const unsigned arow_bytes = (unsigned)(astore_row_stride(gm.G) * sizeof(T));
-    constexpr int lpr = row_bytes / 16, rpd = kLanes / lpr;   // lanes per row, rows per DMA
-#pragma unroll
-    for (int q = 0; q < n; ++q) {
-        const int r = q * rpd + lane / lpr, w = (lane % lpr) * 16;
-        int wo = w;
-        if constexpr (kFoldSwz<T>) {
-            constexpr int blk = 8 * (int)sizeof(T);
-            const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
-            wo = (w / blk) * blk + pc * 16;
-        }
-        const int s0 = ck_step<ALGO>(q * rpd);   // source step of the DMA's first row
-        const int sr = ck_step<ALGO>(r);
-        if (q + 1 < n || q * kDmaBytes + lane * 16 < alpha_dma_bytes<T, ALGO>())
-            dma16_s(lds + q * kDmaBytes, src + (size_t)s0 * arow_bytes, (unsigned)(sr - s0) * arow_bytes + (unsigned)wo);
-    }
-#else   // round-2 form: a 64-bit per-lane source pointer per DMA (contiguous rows only)
-    static_assert(TD_AWIN != 2, "the per-lane form assumes contiguous window rows");
 #pragma unroll
     for (int q = 0; q < n; ++q) {
         const int b = q * kDmaBytes + lane * 16;
@@ -920,9 +695,8 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
             const int pc = ((w % blk) / 16 - av_rot<ALGO>(r, w / blk)) & (kBlkChunks<T> - 1);
             off = ck_step<ALGO>(r) * row_bytes + (w / blk) * blk + pc * 16;
         }
-        if (q + 1 < n || b < alpha_dma_bytes<T, ALGO>()) dma16_pol<TD_ADMA_POLICY>(lds + q * kDmaBytes, src + off);
+        if (q + 1 < n || b < alpha_dma_bytes<T, ALGO>()) dma16_stream(lds + q * kDmaBytes, src + off);
     }
-#endif
 }
 
 // ---- recursion steps
@@ -976,11 +750,7 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
         const LutRow r = lut_row(h.d);
         lut_fields<T>(lut, r.o, h.thr, h.lo, h.hi);
     }
-#ifdef TD_DIAG_SPARSE_ALPHA   // diagnostics only (wrong log-MAP results): the F pass with max-log's stores
-    if ((kCkPhases >> PH) & 1) gstore(pa, alpha);
-#else
-    if (!kArec && ((kCkPh<ALGO> >> PH) & 1)) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
-#endif
+    if ((kCkPh<ALGO> >> PH) & 1) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
     gstore(ptm, m);
     return h;
 }
@@ -1000,8 +770,8 @@ __device__ __forceinline__ T alpha_step(T a, const StepIn<T>& in, const T* lut, 
 
 // beta step i+1 -> i with i mod 3 = PH (log_map.cpp:1004-1021).  beta[.][i+1] (the incoming
 // metric) is published (by state) for the LLR terms of step i by the caller: an LDS store on the
-// chain costs ~45 cycles a step in isolation (ubench_beta), so a full window may store its 12
-// values at its end (TD_BETA_BATCH).
+// chain costs ~45 cycles a step in isolation (ubench_beta), so a full window stores its kW values
+// behind the steps' table reads (BetaSched) or at its end (beta_window).
 template <typename T, int ALGO, int PH>
 __device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc)
 {
@@ -1064,28 +834,13 @@ __device__ __forceinline__ T beta_step_rt(int ph, T beta, const Smem<T>& sm, con
 // next steps' operand reads in front of the row read, or split the row (ds_read2, operand reads,
 // then the row's third read), in every step group.  Reads issued right behind the row read
 // complete in its shadow, long before the next step's row read.
-#ifndef TD_SCHED
-#define TD_SCHED 1
-#endif
 
-// max(xs, xp) + (|d| >= thr ? hi : lo), the max* of a scheduled step.  TD_ADDSEL forms both candidate
-// sums once the row lands and selects between them (one dependent fp64 op less on the chain, one
-// VALU more); the sums are pinned in registers so the compiler cannot fold them back into one add.
-#ifndef TD_ADDSEL
-#define TD_ADDSEL 0
-#endif
+// max(xs, xp) + (|d| >= thr ? hi : lo), the max* of a scheduled step.  (Forming both candidate sums
+// and selecting measured 0.5 % slower: one dependent op less on the chain, one VALU more.)
 template <typename T>
 __device__ __forceinline__ T sched_finish(T xs, T xp, T d, T thr, T lo, T hi)
 {
-    const T mx = vmax(xs, xp);
-    if constexpr (TD_ADDSEL != 0) {
-        T rl = mx + lo, rh = mx + hi;
-        touch(rl);
-        touch(rh);
-        return fabs(d) >= thr ? rh : rl;
-    } else {
-        return mx + (fabs(d) >= thr ? hi : lo);
-    }
+    return vmax(xs, xp) + (fabs(d) >= thr ? hi : lo);
 }
 
 template <typename T, int K>
@@ -1093,7 +848,7 @@ struct AlphaSched {
     // alpha step K (phase K mod 3) of a full window: a = alpha_raw[.][i] in, alpha_raw[.][i+1] out;
     // op[K % 3] holds this step's operands, op[(K + 2) % 3] receives step K+2's
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
-                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0, size_t arow)
+                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -1110,49 +865,32 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!kArec && ((kCkPh<0> >> PH) & 1)) gstore(ga + K * arow + lc.st_off[PH], alpha);   // log-MAP only
+        gstore(ga + K * kLanes + lc.st_off[PH], alpha);   // log-MAP only
         gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
-        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0, arow);
+        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0);
     }
 };
 template <typename T>
 struct AlphaSched<T, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, T*, size_t)
+                                               const LaneConst<T>&, T*, T*, T*)
     {
     }
 };
 
-// AlphaSched for a full window t >= 1 with its scratch stores addressed off wave-uniform bases
-// (TD_SADDR): sa = alpha rows of the window + 6 rows, stm = tempmax rows of the window; va[PH] =
-// this lane's byte offset of its state in a row of phase PH, vtm = its codeword's.  Step K stores
-// alpha at sa + va + (K - kArow0) rows and tempmax[i] at scratch index i - 1 = stm + vtm + (K - 1) rows.
-#ifndef TD_SADDR
-#define TD_SADDR 1
-#endif
-#ifndef TD_LOADER_PRIO_B
-#define TD_LOADER_PRIO_B 0   // VALU priority of the loader wave in the log-MAP B pass
-#endif
-#ifndef TD_LOADER_PRIO_MAXLOG
-#define TD_LOADER_PRIO_MAXLOG 0   // VALU priority of the loader wave in the Max-Log-MAP B pass
-#endif
-#ifndef TD_AOP_FIRST
-#define TD_AOP_FIRST 1
-#endif
-#ifndef TD_SCHED_MAXLOG
-#define TD_SCHED_MAXLOG 1   // fp64 Max-Log-MAP full windows through AlphaSchedS as well: 1930 -> 2050
-                            // Mbit/s on one box; fp32 Max-Log-MAP lost 23 % with it (2380 -> 1827), so
-                            // it keeps alpha_window's pinned step groups
-#endif
-// TD_TM_BATCH: the 8 lanes of a codeword hold the same tempmax, so instead of a store per step each
-// lane keeps the tempmax of one step (lane slot l: steps l and 8 + tm2_slot(l) of the window) and
-// the window writes them with two stores (steps 0-7, then 8..kW-1; lanes whose slots map to one
-// step write the same value twice in the second): 2 scratch stores a window instead of kW.
-#ifndef TD_TM_BATCH
-#define TD_TM_BATCH 1
-#endif
+// AlphaSched for a full window t >= 1 with its scratch stores addressed off wave-uniform bases:
+// sa = alpha rows of the window + kArow0 rows, stm = tempmax rows of the window; va[PH] = this
+// lane's byte offset of its state in a row of phase PH.  Step K stores alpha at sa + va + (K -
+// kArow0) rows.  Log-MAP and fp64 Max-Log-MAP take this path (fp64 Max-Log-MAP 1930 -> 2050 Mbit/s
+// with it; fp32 Max-Log-MAP lost 23 %, so it keeps alpha_window's pinned step groups).
+template <typename T, int ALGO>
+constexpr bool kAlphaSchedS = ALGO == 0 || sizeof(T) == 8;
+// The 8 lanes of a codeword hold the same tempmax, so instead of a store per step each lane keeps
+// the tempmax of one step (lane slot l: steps l and 8 + tm2_slot(l) of the window) and the window
+// writes them with two stores (steps 0-7, then 8..kW-1; lanes whose slots map to one step write the
+// same value twice in the second): 2 scratch stores a window instead of kW.
 static_assert(kW > 8 && kW <= 16, "the tempmax batches cover a window of 8 + (kW - 8) steps");
 // the second batch's step (minus 8) kept by lane slot l
 __host__ __device__ constexpr int tm2_slot(int l) { return kW - 8 == 4 ? (l & 3) : (l < kW - 8 ? l : kW - 9); }
@@ -1163,37 +901,29 @@ struct TmBatch {
     unsigned v1, v2;   // byte offsets of this lane's entry in the first / second batch
 };
 template <typename T, int K>
-__device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm, unsigned vtm)
+__device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm)
 {
-    if constexpr (TD_TM_BATCH) {
-        if constexpr (K < 8)
-            tbh.buf = tbh.slot == K ? m : tbh.buf;
-        else
-            tbh.buf = tm2_slot(tbh.slot) == K - 8 ? m : tbh.buf;
-        if constexpr (K == 7) gstore_s<-kCw * (int)sizeof(T)>(stm, tbh.v1, tbh.buf);           // steps 0-7 at i - 1
-        if constexpr (K == kW - 1) gstore_s<7 * kCw * (int)sizeof(T)>(stm, tbh.v2, tbh.buf);   // steps 8..kW-1
-    } else {
-        gstore_s<(K - 1) * kCw * (int)sizeof(T)>(stm, vtm, m);   // tempmax[i] at scratch index i - 1
-    }
+    if constexpr (K < 8)
+        tbh.buf = tbh.slot == K ? m : tbh.buf;
+    else
+        tbh.buf = tm2_slot(tbh.slot) == K - 8 ? m : tbh.buf;
+    if constexpr (K == 7) gstore_s<-kCw * (int)sizeof(T)>(stm, tbh.v1, tbh.buf);           // steps 0-7 at i - 1
+    if constexpr (K == kW - 1) gstore_s<7 * kCw * (int)sizeof(T)>(stm, tbh.v2, tbh.buf);   // steps 8..kW-1
 }
 
-// alpha row K of a full window: wave-uniform base sa in SGPRs, per-lane byte offset voff.  Window-
-// and group-major layouts (TD_AWIN 0, 1): sa = row kArow0 of the window and the row is an immediate offset
-// (no per-step address arithmetic); step-major (TD_AWIN 2): sa = row 0, rows arow elements apart.
+// alpha row K of a full window: wave-uniform base sa (row kArow0 of the window) in SGPRs, per-lane
+// byte offset voff, the row an immediate offset (no per-step address arithmetic)
 template <typename T, int K>
-__device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v, size_t arow)
+__device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v)
 {
-    if constexpr (TD_AWIN == 2)
-        gstore_s<0>(sa + K * arow, voff, v);
-    else
-        gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
+    gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
 }
 
 template <typename T, int ALGO, int K>
 struct AlphaSchedS {
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
                                                int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
-                                               unsigned vtm, TmBatch<T>& tbh, size_t arow)
+                                               TmBatch<T>& tbh)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -1211,11 +941,8 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-#ifdef TD_DIAG_SPARSE_ASCHED   // diagnostics only (wrong log-MAP results): alpha stored at phase 0 only
-            if constexpr (PH == 0)
-#endif
-            if constexpr (!kArec && ((kCkPh<ALGO> >> PH) & 1)) astore_row<T, K>(sa, va[PH], alpha, arow);
-            tm_keep<T, K>(tbh, m, stm, vtm);
+            astore_row<T, K>(sa, va[PH], alpha);
+            tm_keep<T, K>(tbh, m, stm);
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
         } else {
@@ -1223,30 +950,26 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!kArec && ((kCkPh<ALGO> >> PH) & 1)) astore_row<T, K>(sa, va[PH], alpha, arow);
-            tm_keep<T, K>(tbh, m, stm, vtm);
+            if constexpr ((kCkPh<ALGO> >> PH) & 1) astore_row<T, K>(sa, va[PH], alpha);
+            tm_keep<T, K>(tbh, m, stm);
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
         }
-        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh, arow);
+        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh);
     }
 };
 template <typename T, int ALGO>
 struct AlphaSchedS<T, ALGO, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], unsigned, TmBatch<T>&,
-                                               size_t)
+                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], TmBatch<T>&)
     {
     }
 };
 static_assert(kArow0 * kLanes * 8 <= 4096 && (kW - 1 - kArow0) * kLanes * 8 < 4096, "scheduled alpha store offsets fit the immediate");
 
-// TD_BETA_SHADOW: each beta step writes its incoming beta[.][i+1] (the fold input of step i) into
-// the window's Bv rows behind its own row read, instead of the 12 writes (and their rotated
-// addresses) after the window, which the chain waited for at the window's barrier.
-#ifndef TD_BETA_SHADOW
-#define TD_BETA_SHADOW 1
-#endif
+// Each beta step writes its incoming beta[.][i+1] (the fold input of step i) into the window's Bv
+// rows behind its own row read, instead of the kW writes (and their rotated addresses) after the
+// window, which the chain waited for at the window's barrier.
 
 template <typename T, int K>
 struct BetaSched {
@@ -1269,7 +992,7 @@ struct BetaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K >= 2) op[(K + 1) % 3] = beta_in<T, (K - 2) % 3>(sm, tb, K - 2, c, lc, tmw);
         __builtin_amdgcn_sched_barrier(0);
-        if (TD_BETA_SHADOW) Bvw[K * kLanes + rot_off<T>(lc.st_off[(K + 1) % 3], K)] = bs[K];
+        Bvw[K * kLanes + rot_off<T>(lc.st_off[(K + 1) % 3], K)] = bs[K];
         __builtin_amdgcn_sched_barrier(0);
         beta = sched_finish(xs, xp, d, thr, lo, hi) - in.tm;   // :1012-1019
         BetaSched<T, K - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
@@ -1289,25 +1012,23 @@ struct BetaSched<T, -1> {
 // stores tempmax[L] after the last window.
 template <typename T, int ALGO>
 __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, const T* lut, int c,
-                                          const LaneConst<T>& lc, T* ga, T* gtm, size_t arow,
+                                          const LaneConst<T>& lc, T* ga, T* gtm,
                                           unsigned long long* chain_st = nullptr)
 {
     (void)chain_st;
+    constexpr size_t arow = kLanes;   // rows of a window, arow elements apart
     const int tb = t % 3;
-    if constexpr (kArec) gstore(ga + lc.st_off[0], a);   // checkpoint: alpha_raw entering the window (row 0)
-#if TD_SCHED
     if constexpr (ALGO == 0) {
         if (n == kW) {
             StepIn<T> op[3];
             op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
             op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
             TD_CHAIN_T0(c0);
-            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0), arow);
+            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0));
             TD_CHAIN_ACC(c0);
             return a;
         }
     }
-#endif
     T* pa0 = ga + lc.st_off[0];
     T* pa1 = ga + arow + lc.st_off[1];
     T* pa2 = ga + 2 * arow + lc.st_off[2];
@@ -1356,115 +1077,11 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
     return a;
 }
 
-// ------------------------------------------------------------------ alpha recompute (TD_AREC)
-#ifndef TD_AREC_PRIO
-#define TD_AREC_PRIO 2   // VALU priority of wave R in the B pass (beta's is TD_BETA_PRIO_*)
-#endif
-#ifndef TD_AREC_ROLES
-#define TD_AREC_ROLES 1   // wg_pos: R on wave 2, the loader on wave 4
-#endif
-// Wave R, B pass: alpha over window t again, from the F pass's checkpoint (alpha_raw entering the
-// window's first step, stored by wave A at row 0 of the window's scratch), with wave A's arithmetic
-// step for step (alpha_tempmax, the two fma, the table max*: bit-identical), publishing alpha[.][i]
-// of every step by state into the Av ring (rotated blocks, as beta publishes Bv) instead of HBM.
-template <typename T, int ALGO, int PH>
-__device__ __forceinline__ T arec_step(T a, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc, T* Avw, int k)
-{
-    T an;
-    const T m = alpha_tempmax<T, PH>(a, an);
-    const T alpha = a - m, ap = an - m;
-    const T xs = fma(lc.a_sg[PH], in.gs, alpha);
-    const T xp = fma(lc.a_pg[PH], in.gp, ap);
-    if constexpr (ALGO == 0) {
-        const T d = xp - xs;
-        const LutRow r = lut_row(d);
-        T thr, lo, hi;
-        lut_fields<T>(lut, r.o, thr, lo, hi);
-        Avw[k * kLanes + rot_off<T>(lc.st_off[PH], k)] = alpha;   // behind the table read
-        return sched_finish(xs, xp, d, thr, lo, hi);
-    } else {
-        Avw[k * kLanes + rot_off<T>(lc.st_off[PH], k)] = alpha;
-        return vmax(xs, xp);
-    }
-}
-
-// a full window, scheduled like AlphaSchedS: [chain to the row address] [row reads] [operand reads
-// of step K+2] [the Av write] [select + add]
-template <typename T, int ALGO, int K>
-struct AlphaSchedR {
-    static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
-                                               int c, const LaneConst<T>& lc, T* Avw)
-    {
-        constexpr int PH = K % 3;
-        const StepIn<T> in = op[K % 3];
-        T an;
-        const T m = alpha_tempmax<T, PH>(a, an);
-        const T alpha = a - m, ap = an - m;
-        const T xs = fma(lc.a_sg[PH], in.gs, alpha);
-        const T xp = fma(lc.a_pg[PH], in.gp, ap);
-        if constexpr (ALGO == 0) {
-            const T d = xp - xs;
-            const LutRow r = lut_row(d);
-            __builtin_amdgcn_sched_barrier(0);
-            T thr, lo, hi;
-        lut_fields<T>(lut, r.o, thr, lo, hi);
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
-            __builtin_amdgcn_sched_barrier(0);
-            Avw[K * kLanes + rot_off<T>(lc.st_off[PH], K)] = alpha;
-            __builtin_amdgcn_sched_barrier(0);
-            a = sched_finish(xs, xp, d, thr, lo, hi);
-        } else {
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
-            __builtin_amdgcn_sched_barrier(0);
-            Avw[K * kLanes + rot_off<T>(lc.st_off[PH], K)] = alpha;
-            __builtin_amdgcn_sched_barrier(0);
-            a = vmax(xs, xp);
-        }
-        AlphaSchedR<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, Avw);
-    }
-};
-template <typename T, int ALGO>
-struct AlphaSchedR<T, ALGO, kW> {
-    static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*)
-    {
-    }
-};
-
-// alpha of the n steps of window t (G ring slot tb) from its checkpoint a, into Avw = Av[t & 1]
-template <typename T, int ALGO>
-__device__ __forceinline__ void arec_window(T a, int tb, int n, const Smem<T>& sm, const T* lut, int c,
-                                            const LaneConst<T>& lc, T* Avw)
-{
-    if (n == kW) {
-        StepIn<T> op[3];
-        op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
-        op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
-        __builtin_amdgcn_sched_barrier(0);
-        AlphaSchedR<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, Avw);
-        return;
-    }
-    for (int k = 0; k < n; k += 3) {   // the last window (window starts are = 0 mod 3)
-        a = arec_step<T, ALGO, 0>(a, alpha_in<T, 0>(sm, tb, k, c, lc), lut, lc, Avw, k);
-        if (k + 1 < n) a = arec_step<T, ALGO, 1>(a, alpha_in<T, 1>(sm, tb, k + 1, c, lc), lut, lc, Avw, k + 1);
-        if (k + 2 < n) a = arec_step<T, ALGO, 2>(a, alpha_in<T, 2>(sm, tb, k + 2, c, lc), lut, lc, Avw, k + 2);
-    }
-}
-
-#ifndef TD_BETA_BATCH
-#define TD_BETA_BATCH 1
-#endif
-#ifndef TD_BETA_PIN
-#define TD_BETA_PIN 1
-#endif
-constexpr bool kBetaBatch = TD_BETA_BATCH != 0;   // beta published once per window, not per step
 // operand prefetch pinned behind a table read (A/B on one box, config 2: fp64 1192 -> 1207
 // Mbit/s).  fp32 log-MAP lost with it before its table went to 32 columns (1461 -> 1436) and gains
 // with it since (with beta at priority 2: 1414 -> 1443); fp32 Max-Log-MAP still loses (-0.4 %).
 template <typename T, int ALGO>
-constexpr bool kBetaPin = TD_BETA_PIN != 0 && (sizeof(T) == 8 || ALGO == 0);
+constexpr bool kBetaPin = sizeof(T) == 8 || ALGO == 0;
 
 // beta over the n steps of window t, downwards (full windows: static phases; else runtime).
 // FULL = false keeps only the rolled runtime-phase loop (the last window in the dedicated loop of
@@ -1485,29 +1102,20 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
         }
         return beta;
     }
-#if TD_SCHED
     if (ALGO == 0 && n == kW) {
-        T bs[kW];   // beta[.][i+1] of step k, published after the window
+        T bs[kW];   // beta[.][i+1] of step k (BetaSched publishes it behind the step's row read)
         StepIn<T> op[3];
         op[(kW - 1) % 3] = beta_in<T, (kW - 1) % 3>(sm, tb, kW - 1, c, lc, tmw);
         op[(kW - 2) % 3] = beta_in<T, (kW - 2) % 3>(sm, tb, kW - 2, c, lc, tmw);
         TD_CHAIN_T0(c0);
         BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
         TD_CHAIN_ACC(c0);
-        if (!TD_BETA_SHADOW)
-#pragma unroll
-            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
         return beta;
     }
-#endif
     if (n == kW) {
-        T bs[kW];   // beta[.][i+1] of step k, stored by lane after the window (TD_BETA_BATCH)
-        auto put = [&](int k, T v) {
-            if (kBetaBatch)
-                bs[k] = v;
-            else
-                Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = v;
-        };
+        T bs[kW];   // beta[.][i+1] of step k, stored by lane after the window (an LDS store per step on
+                    // the chain costs ~45 cycles a step in isolation, ubench_beta)
+        auto put = [&](int k, T v) { bs[k] = v; };
         // operands read one step group ahead (the next group's inputs load under this group's chain)
         StepIn<T> b2 = beta_in<T, 2>(sm, tb, kW - 1, c, lc, tmw);
         StepIn<T> b1 = beta_in<T, 1>(sm, tb, kW - 2, c, lc, tmw);
@@ -1517,7 +1125,7 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
             const int kn = k >= 3 ? k - 3 : k;
             put(k, beta);
             const StepHalf<T> h = beta_issue<T, ALGO, 2>(beta, b2, lut, lc);
-            // the next group's operands, issued right behind this step's table read (TD_BETA_PIN)
+            // the next group's operands, issued right behind this step's table read (kBetaPin)
             if (kBetaPin<T, ALGO>) __builtin_amdgcn_sched_barrier(0);
             const StepIn<T> n2 = beta_in<T, 2>(sm, tb, kn, c, lc, tmw);
             const StepIn<T> n1 = beta_in<T, 1>(sm, tb, kn - 1, c, lc, tmw);
@@ -1532,9 +1140,8 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
             b1 = n1;
             b0 = n0;
         }
-        if (kBetaBatch)
 #pragma unroll
-            for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
+        for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
     } else {
         for (int k = n - 1; k >= 0; --k) {
             const int ph1 = (k + 1) % 3;   // constant indices only: a runtime index into lc moves it to scratch
@@ -1546,10 +1153,7 @@ __device__ __forceinline__ T beta_window(T beta, int t, int n, Smem<T>& sm, cons
 }
 
 // beta_window's scheduled path for a full window whose ring slots the caller keeps as running
-// counters (tb = t % 3, xb = t & 1): no window-length test, no modular arithmetic (TD_BETA_FAST)
-#ifndef TD_BETA_FAST
-#define TD_BETA_FAST 1
-#endif
+// counters (tb = t % 3, xb = t & 1): no window-length test, no modular arithmetic
 template <typename T, int ALGO>
 __device__ __forceinline__ T beta_window_full(T beta, int tb, int xb, Smem<T>& sm, const T* lut, int c,
                                               const LaneConst<T>& lc, unsigned long long* chain_st = nullptr)
@@ -1564,9 +1168,6 @@ __device__ __forceinline__ T beta_window_full(T beta, int tb, int xb, Smem<T>& s
     TD_CHAIN_T0(c0);
     BetaSched<T, kW - 1>::run(beta, op, bs, sm, tb, lut, c, lc, tmw, Bvw);
     TD_CHAIN_ACC(c0);
-    if (!TD_BETA_SHADOW)
-#pragma unroll
-        for (int k = 0; k < kW; ++k) Bvw[k * kLanes + rot_off<T>(lc.st_off[(k + 1) % 3], k)] = bs[k];
     return beta;
 }
 
@@ -1598,25 +1199,6 @@ __device__ __forceinline__ void alpha_recompute(T (&a)[8], T P, T Q, const T* lu
     for (int j = 0; j < 8; ++j) a[j] = n[j] - m;
 }
 
-// TD_AV_DIRECT: the alpha block of (window t, row r, codeword c) in the HBM scratch, and its 8
-// states loaded into registers (one 16-byte load per chunk; the scratch rows are by 8c + state)
-template <typename T>
-__device__ __forceinline__ const T* av_global(const T* astore, const Geom& gm, int t, int r, int c)
-{
-    return astore + astore_window_off(gm.g, t, gm.G, gm.L) + (size_t)r * astore_row_stride(gm.G) + c * 8;
-}
-template <typename T>
-__device__ __forceinline__ void load_block_global(const T* p, T (&v)[8])
-{
-    constexpr int E = 16 / (int)sizeof(T);
-    using V = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
-#pragma unroll
-    for (int q = 0; q < kBlkChunks<T>; ++q) {
-        const V x = *reinterpret_cast<const V*>(p + q * E);
-        __builtin_memcpy(&v[q * E], &x, 16);
-    }
-}
-
 // LLR fold + extrinsic + outputs of item e = k*8 + c of window t (:1024-1039, :1234-1264):
 //   temp_u[j] = (gamma[p][i][u] + alpha[p][i]) + beta[j][i+1],  p = laststat[j][u],
 //   LLR = E_seq(temp1) - E_seq(temp0)
@@ -1624,7 +1206,7 @@ __device__ __forceinline__ void load_block_global(const T* p, T (&v)[8])
 // reference's (gamma + alpha) + beta.  Both folds run in the same lane (independent chains).
 template <typename T, int ALGO>
 __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t, int e, const SisoDst<T>& dst,
-                                          const Geom& gm, const T* astore)
+                                          const Geom& gm)
 {
     const int k = e >> 3, c = e & 7;
     const int i = t * kW + k;
@@ -1639,18 +1221,12 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
         // exactly as the alpha wave computed them (:975-1001)
         int ks;
         const int r = ck_row_of<ALGO>(k, ks);
-        if constexpr (kAvDirect) {
-            load_block_global<T>(av_global(astore, gm, t, ks, c), a);   // the scratch keeps rows at their steps
-        } else {
-            const T* av = &sm.Av[t % kAvSlots][r][c * 8];
-            load_block<T>(av, av_rot<ALGO>(r, c), a);
-        }
+        const T* av = &sm.Av[t % kAvSlots][r][c * 8];
+        load_block<T>(av, av_rot<ALGO>(r, c), a);
         for (int s = ks; s < k; ++s) {
             const T* gs = &sm.G[t % 3][s][c][0];
             alpha_recompute<T, ALGO>(a, gs[0], gs[1], lut);
         }
-    } else if constexpr (kAvDirect) {
-        load_block_global<T>(av_global(astore, gm, t, k, c), a);
     } else {
         const T* av = &sm.Av[t % kAvSlots][k][c * 8];
         load_block<T>(av, k, a);
@@ -1691,13 +1267,10 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     }
 }
 
-// fold_item for the turbo decode's full windows (TD_FOLD_FAST): the lane's LDS rows and output
-// bases are set up once per SISO, the window enters only as its ring slots (s3 = t % 3, s4 = t %
-// kAvSlots, s2 = t & 1, kept as running counters by the caller) and its first step i0.  Extrinsic
-// written permuted (ext_mode 2 / 3), no raw-LLR or Le dump (those take fold_item).
-#ifndef TD_FOLD_FAST
-#define TD_FOLD_FAST 1
-#endif
+// fold_item for the turbo decode's full windows: the lane's LDS rows and output bases are set up
+// once per SISO, the window enters only as its ring slots (s3 = t % 3, s4 = t % kAvSlots, s2 = t &
+// 1, kept as running counters by the caller) and its first step i0.  Extrinsic written permuted
+// (ext_mode 2 / 3), no raw-LLR or Le dump (those take fold_item).
 template <typename T>
 struct FoldLane {
     int k, c;
@@ -1713,7 +1286,7 @@ struct FoldLane {
 };
 template <typename T, int ALGO>
 __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* lut, int s3, int s4, int s2, int i0,
-                                               int ext_len, int K, const T (&ain)[8])
+                                               int ext_len, int K)
 {
     const int k = fl.k;
     const T* g = fl.G + s3 * (kW * kCw * 4);
@@ -1722,12 +1295,7 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const int wperm = wp[0], wbit = wp[1];
     T a[8], b[8], t0[8], t1[8];
     load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
-    if constexpr (kAvDirect) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = ain[j];   // loaded one window ahead (siso_wg)
-    } else {
-        load_block<T>(fl.Av + s4 * (kW * kLanes), kFoldRows<ALGO> ? k : fl.arot, a);
-    }
+    load_block<T>(fl.Av + s4 * (kW * kLanes), kFoldRows<ALGO> ? k : fl.arot, a);
     if constexpr (!kFoldRows<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
         const T* gr = fl.Gr + s3 * (kW * kCw * 4);
         for (int q = 0; q < fl.rec; ++q) alpha_recompute<T, ALGO>(a, gr[q * kCw * 4], gr[q * kCw * 4 + 1], lut);
@@ -1738,12 +1306,6 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
         t0[j] = (a[p0] - (kTrellisQ[p0] ? Q : P)) + b[j];   // u = 0: gamma = -(P|Q)
         t1[j] = (a[p1] + (kTrellisQ[p1] ? Q : P)) + b[j];   // u = 1: gamma = +(P|Q)
     }
-#ifdef TD_DIAG_HALFFOLD   // diagnostics only (wrong results): one E_seq chain per item
-    T r0 = mstar<T, ALGO>(t0[0], t1[1], lut);
-#pragma unroll
-    for (int j = 2; j < 8; ++j) r0 = mstar<T, ALGO>(r0, t0[j] + t1[j], lut);
-    const T r1 = P;
-#else
     T r0, r1;
     if constexpr (ALGO == 1) {   // Max-Log-MAP: a max tree (exact in any order), as fold_item
         r0 = vmax(vmax(vmax(t0[0], t0[1]), vmax(t0[2], t0[3])), vmax(vmax(t0[4], t0[5]), vmax(t0[6], t0[7])));
@@ -1757,55 +1319,11 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
             r1 = mstar<T, ALGO>(r1, t1[j], lut);
         }
     }
-#endif
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
     const int i = i0 + k;
     if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
     if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
-}
-
-// fold_item_fast with one E_seq chain per lane (TD_FOLD_SPLIT, wave F1): lane l < 32 folds temp0 of
-// the item (fl.k, fl.c), lane l + 32 temp1 of the same item.  temp1[j] = (alpha[p1(j)] + G) + beta[j]
-// and temp0[j] = (alpha[p0(j)] - G) + beta[j] use the same G = P|Q (kTrellisQ[p0(j)] ==
-// kTrellisQ[p1(j)]) and p1(j) = p0(j) ^ 1, so the temp1 lanes read their alpha block with the two
-// states of each pair swapped and both halves run one instruction stream: fma(+-1, G, alpha) + beta
-// (fma(-1, G, a) = a - G exactly), then the chain.  Called by all 64 lanes (the exchange needs them).
-template <typename T, int ALGO>
-__device__ __forceinline__ void fold_item_split(const FoldLane<T>& fl, const T* lut, int s3, int s4, int s2, int i0,
-                                                int ext_len, int K, int u, bool active)
-{
-    const int k = fl.k;
-    const T* g = fl.G + s3 * (kW * kCw * 4);
-    const T P = g[0], Q = g[1], ys = g[2], la = g[3];
-    const int* wp = fl.Wp + s3 * (kW * 2);
-    const int wperm = wp[0], wbit = wp[1];
-    T a[8], b[8], t[8];
-    load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
-    // alpha state s ^ u into a[s], read at its own address (the pair's two states are adjacent in
-    // the block: blk_off(s ^ 1) = blk_off(s) ^ 1); u opaque, so the compiler reads, not selects
-    int ux = u;
-    touch(ux);
-    const T* av = fl.Av + s4 * (kW * kLanes);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = av[blk_off<T>(q, k) ^ ux];
-    const T sg = u ? (T)1 : (T)-1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int p0 = kTrellisLast[j][0];
-        t[j] = fma(sg, kTrellisQ[p0] ? Q : P, a[p0]) + b[j];   // a[p0] = alpha[p1(j)] in the temp1 lanes
-    }
-    T r = mstar<T, ALGO>(t[0], t[1], lut);
-#pragma unroll
-    for (int j = 2; j < 8; ++j) r = mstar<T, ALGO>(r, t[j], lut);
-    const T r1 = __shfl_xor(r, 32);   // lanes l < 32: temp1's fold from lane l + 32
-    if (u == 0 && active) {
-        const T llr = r1 - r;
-        const T le = llr - la - (T)2 * ys;
-        const int i = i0 + k;
-        if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
-        if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
-    }
 }
 
 #ifdef TD_STAMPS
@@ -1816,27 +1334,16 @@ __device__ __forceinline__ void fold_item_split(const FoldLane<T>& fl, const T* 
 #define TD_STAMP(v)
 #define TD_ACC(slot, a, b)
 #endif
-#ifndef TD_ALPHA_PRIO
-#define TD_ALPHA_PRIO 2   // VALU priority of the alpha wave in the F pass
-#endif
-// TD_LOADER_REMAT: the loader's per-lane DMA addresses are rebuilt in every iteration (the lane index
-// made opaque to the compiler there) instead of being hoisted out of the passes and kept live: the
-// hoisted addresses set the kernel's register count (the loader is the role with the most live VGPRs)
-#ifndef TD_LOADER_REMAT
-#define TD_LOADER_REMAT 0
-#endif
-// TD_ROLE_REMAT: the lane index made opaque at the start of every SISO, so that the compiler cannot
+constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
+// The lane index made opaque at the start of every SISO (role remat), so that the compiler cannot
 // hoist the roles' lane-derived addresses (fold lanes, alpha store offsets, ...) out of the SISO loop,
 // where they were all live at once, in every role: fp64 log-MAP 256 -> 95 VGPRs, fp32 log-MAP 191 ->
-// 78, so that three workgroups fit a CU (turbo_decode_kernel3).  1 (default): fp32, and fp64 with
+// 78, so that three workgroups fit a CU (turbo_decode_kernel3).  On for fp32, and for fp64 with
 // 15-step windows (without it that build spills to scratch) -- with 12-step windows at two
 // workgroups per CU it measured level in fp64 log-MAP (17.39 vs 17.40 ms) and 1.4 % slower in fp64
-// Max-Log-MAP; 2: both precisions; 0: off.
-#ifndef TD_ROLE_REMAT
-#define TD_ROLE_REMAT 1
-#endif
+// Max-Log-MAP.
 template <typename T>
-constexpr bool kRoleRemat = TD_ROLE_REMAT == 2 || (TD_ROLE_REMAT == 1 && (sizeof(T) == 4 || kW != 12));
+constexpr bool kRoleRemat = sizeof(T) == 4 || kW != 12;
 constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
                                  // barriers, F prologue, loader B prologue, loader first tile (see diag)
@@ -1854,18 +1361,13 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                         T* tmstore, const LaneTables* lt, int wave, int lane, unsigned long long* st)
 {
     (void)st;
-    if constexpr (kRoleRemat<T>) touch(lane);   // nothing derived from the lane index is SISO-invariant (TD_ROLE_REMAT)
+    if constexpr (kRoleRemat<T>) touch(lane);   // nothing derived from the lane index is SISO-invariant (role remat)
     TD_STAMP(p0);
     const int nT = gm.nT;
     const int tl = nT - 1;
     const int nB = nT + 2;   // B-pass iterations: j = 0 .. nT+1 (wa = tl - j, wb = wa + 1, wf = wa + 2)
-    T* ga0 = astore + astore_window_off(gm.g, 0, gm.G, gm.L);   // row 0 of window 0 of this group
-    const size_t aws = astore_window_stride(gm.G);                // window t starts at ga0 + t * aws
-#if TD_AWIN == 2
-    const size_t arow = astore_row_stride(gm.G);                  // rows of a window, arow elements apart
-#else
-    constexpr size_t arow = kLanes;                               // rows of a window, arow elements apart
-#endif
+    T* ga0 = astore + astore_window_off(gm.g, 0, gm.L);   // row 0 of window 0 of this group
+    constexpr size_t aws = (size_t)kW * kLanes;            // window t starts at ga0 + t * aws
     T* gtm0 = tmstore + (size_t)gm.g * gm.L * kCw;
 
     // ===================================== F pass
@@ -1874,26 +1376,16 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
         T a = lc.a_init0 ? (T)0 : (T)-kInfty;   // alpha[.][0] (:943,948), its tempmax is 0
-        __builtin_amdgcn_s_setprio(TD_ALPHA_PRIO);
+        __builtin_amdgcn_s_setprio(kAlphaPrio);
         wg_sync_lds();
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
-#ifdef TD_DIAG_FPAIR   // diagnostics only (wrong results): two alpha windows per F-pass barrier (on one tile)
-        for (int t = 0; t < nT; t += 2) {
-            TD_STAMP(f0);
-            a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                      ga0 + (size_t)t * aws, gtm0 + (size_t)t * kW * kCw, arow, st ? st + 4 : nullptr);
-            if (t + 1 < nT)
-                a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                          ga0 + (size_t)(t + 1) * aws, gtm0 + (size_t)(t + 1) * kW * kCw, arow,
-                                          st ? st + 4 : nullptr);
-#else
         int t0 = 0;
-        if constexpr ((ALGO == 0 || (TD_SCHED_MAXLOG && sizeof(T) == 8)) && TD_SCHED && TD_SADDR) {
+        if constexpr (kAlphaSchedS<T, ALGO>) {
             // windows 1 .. tl-1 are full: running bases and slot index, no per-window address math
             if (tl >= 2) {
                 TD_STAMP(f0);
-                a = alpha_window<T, ALGO>(a, 0, kW, sm, lut_col(sm, lane), c, lc, ga0, gtm0, arow, st ? st + 4 : nullptr);
+                a = alpha_window<T, ALGO>(a, 0, kW, sm, lut_col(sm, lane), c, lc, ga0, gtm0, st ? st + 4 : nullptr);
                 TD_STAMP(f1);
                 wg_sync_lds();
                 TD_STAMP(f2);
@@ -1901,10 +1393,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 TD_ACC(1, f1, f2);
                 const unsigned va[3] = {(unsigned)(lc.st_off[0] * sizeof(T)), (unsigned)(lc.st_off[1] * sizeof(T)),
                                         (unsigned)(lc.st_off[2] * sizeof(T))};
-                const unsigned vtm = (unsigned)(c * sizeof(T));
                 TmBatch<T> tbh{(T)0, lane & 7, (unsigned)(((lane & 7) * kCw + c) * sizeof(T)),
                                (unsigned)((tm2_slot(lane & 7) * kCw + c) * sizeof(T))};
-                T* sa = ga0 + aws + (TD_AWIN == 2 ? 0 : (size_t)kArow0 * kLanes);   // window 1, row kArow0 (row 0: astore_row)
+                T* sa = ga0 + aws + (size_t)kArow0 * kLanes;   // window 1, row kArow0 (astore_row)
                 T* stm = gtm0 + (size_t)kW * kCw;
                 const T* lut = lut_col(sm, lane);
                 unsigned long long* chain_st = st ? st + 4 : nullptr;
@@ -1915,10 +1406,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     StepIn<T> op[3];
                     op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
-                    if (TD_AOP_FIRST) __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
-                    if constexpr (kArec) astore_row<T, 0>(sa, va[0], a, arow);   // checkpoint (row 0)
+                    __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
                     TD_CHAIN_T0(c0);
-                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, vtm, tbh, arow);
+                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh);
                     TD_CHAIN_ACC(c0);
                     sa += aws;
                     stm += (size_t)kW * kCw;
@@ -1934,9 +1424,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         for (int t = t0; t < nT; ++t) {
             TD_STAMP(f0);
-            a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc,
-                                      ga0 + (size_t)t * aws, gtm0 + (size_t)t * kW * kCw, arow, st ? st + 4 : nullptr);
-#endif
+            a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc, ga0 + (size_t)t * aws,
+                                      gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
             if (t == tl) {
                 gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
@@ -1951,25 +1440,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     } else if (wave == 2) {
         // Loader: every input travels HBM -> LDS by DMA into a staging slot, and this wave converts
         // landed slots into the ring (no VGPR is ever the target of a load in flight).
-        [[maybe_unused]] const int lane_in = lane;
         // Invariant: every iteration ends with a wait that leaves only its own DMAs in flight.
         // F pass iteration t: convert window t+1 (staged two iterations ago, slot (t+1) % 3) and
         // stage window t+3 into slot t % 3, which window t left one iteration ago.
         constexpr int kF = kTileDma<T>;
         auto fstep = [&](int t) {
             TD_STAMP(f0);
-#if TD_LOADER_REMAT
-            int lane = lane_in;   // opaque per iteration: the DMA addresses are rebuilt, not kept live
-            touch(lane);
-#endif
-#ifdef TD_DIAG_NOCONVERT   // diagnostics only (wrong results): the F pass without the loader's LDS
-            // traffic but for the last three windows, whose tiles (write positions) the B pass uses
-            if (t + 1 <= tl && t + 1 >= tl - 2) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
-            if (min(t + 3, tl) >= tl - 2) tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
-#else
             if (t + 1 <= tl) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
             tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
-#endif
             vm_wait<kF>();   // window t+2 has landed
             TD_STAMP(f1);
             wg_sync_lds();
@@ -1988,11 +1466,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         wg_sync_lds();
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
-#ifdef TD_DIAG_FPAIR
-        for (int t = 0; t < nT; t += 2) fstep(t);
-#else
         for (int t = 0; t < nT; ++t) fstep(t);
-#endif
         // B pass iteration j (wa = tl - j) converts the tiles of wa (tiles tl-2..tl never left the
         // ring) and tempmax of wa (beta, next iteration) from staging slot j % 3 into the LDS slots
         // nobody reads this iteration, stages the same streams three windows lower into the slot it
@@ -2000,40 +1474,18 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // (last read at j-1).  All DMAs are unconditional (clamped windows, a spare slot at the
         // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
         // own and the previous iteration's DMAs in flight: three windows of latency for each.
-#ifdef TD_DIAG_NOADMA   // diagnostics only (wrong results): the B pass without the loader's alpha copies
-        constexpr int kAd = 0;
-#else
-        constexpr int kAd = alpha_dma_count<T, ALGO>();
-#endif
+        constexpr int kAd = kDiag<kDiagNoAdma> ? 0 : alpha_dma_count<T, ALGO>();
         constexpr int kB = kF + 1 + kAd;
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
-        if constexpr (ALGO == 1) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_MAXLOG);   // Max-Log-MAP: the loader bounds the B pass
-        if constexpr (ALGO == 0 && TD_LOADER_PRIO_B) __builtin_amdgcn_s_setprio(TD_LOADER_PRIO_B);
         auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
-#if TD_LOADER_REMAT
-            int lane = lane_in;
-            touch(lane);
-#endif
             const int wa = tl - j;
-#ifndef TD_DIAG_NOBCONVERT   // diagnostics only (wrong results): no B-pass converts (tiles stay as staged)
-            if constexpr (TD_CONVERT_BATCH != 0) {
-                if (wa >= 0) bpass_convert(sm, slot, src, wa, lane, wa <= tl - 3, true);
-            } else {
+            if constexpr (!kDiag<kDiagNoBConvert>) {
                 if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 if (wa >= 0) tm_convert(sm, slot, wa, lane);
             }
-#endif
-#ifdef TD_STAMPS_LOADER   // diagnostic split of the loader's B-pass work (slots 11: converts, 13: their drain)
-            TD_STAMP(bc);
-            TD_ACC(11, b0, bc);
-#endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
-#ifdef TD_STAMPS_LOADER
-            TD_STAMP(bl);
-            TD_ACC(13, bc, bl);
-#endif
             tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
             tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
             if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
@@ -2063,12 +1515,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
         return;
-    } else if (dst.sys2_out && wave != 4) {
+    } else if (dst.sys2_out) {
         // waves 1 and 3, first SISO: SISO2's systematic input sys2[g][i][c] = sys1[g][pi(i)][c]
-        // (i < K; :1109-1113), one element of window t per lane (96 of 128 lanes) with pi(i) from
-        // the ring slot of window t (Wp[.][k][1], staged by the loader), loaded in iteration t
-        // and stored in t+1, so no wave ever waits on HBM before a barrier.  This is
-        // demux_perm_kernel's work, done by the waves the F pass leaves idle.
+        // (i < K; :1109-1113), one element of window t per lane (kTile - 64 of 128 lanes in the
+        // second wave) with pi(i) from the ring slot of window t (Wp[.][k][1], staged by the
+        // loader), loaded in iteration t and stored in t+1, so no wave ever waits on HBM before a
+        // barrier.  This is demux_perm_kernel's work, done by the waves the F pass leaves idle.
         wg_sync_lds();
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
@@ -2099,11 +1551,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         wg_sync_lds();   // waves 1 and 3 idle in the F pass: keep the barrier count
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
-#ifdef TD_DIAG_FPAIR
-        for (int t = 0; t < nT; t += 2) {
-#else
         for (int t = 0; t < nT; ++t) {
-#endif
             TD_STAMP(f0);
             TD_STAMP(f1);
             wg_sync_lds();
@@ -2113,39 +1561,15 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     }
 
-    // ===================================== B pass (waves 0, 1, 3; 4 with TD_AREC)
-    if (kArec && wave == 4) {
-        // R: alpha over window wb = tl - j + 1 (beta's window) into Av[wb & 1], folded next
-        // iteration; the checkpoint of the next window is loaded one iteration ahead
-        const int c = lane >> 3;
-        LaneConst<T> lc;
-        lane_setup(lt, lane, lc);
-        const T* lut = lut_col(sm, lane);
-        const int cko = lc.st_off[0];
-        T ck = ga0[(size_t)tl * aws + cko];
-        __builtin_amdgcn_s_setprio(TD_AREC_PRIO);
-        for (int j = 0; j < nB; ++j) {
-            TD_STAMP(b0);
-            const int wb = tl - j + 1;
-            if (wb >= 0 && wb <= tl) {
-                const T cn = ga0[(size_t)max(wb - 1, 0) * aws + cko];
-                arec_window<T, ALGO>(ck, wb % 3, window_len(gm, wb), sm, lut, c, lc, &sm.Av[wb & 1][0][0]);
-                ck = cn;
-            }
-            TD_STAMP(b1);
-            wg_sync_lds();
-            TD_STAMP(b2);
-            TD_ACC(2, b0, b1);
-            TD_ACC(3, b1, b2);
-        }
-    } else if (wave == 1) {
+    // ===================================== B pass (waves 0, 1, 3)
+    if (wave == 1) {
         // beta over window wb = tl - j + 1 (its tempmax was staged last iteration)
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
         const int phL = gm.L % 3;   // beta[.][L] lives in the labeling of phase L mod 3
         T beta = (src.terminated && !((lc.b_init0 >> phL) & 1)) ? (T)-kInfty : (T)0;   // :944,951-959
         int j0 = 0;
-        if constexpr (ALGO == 0 && TD_SCHED && TD_BETA_FAST) {
+        if constexpr (ALGO == 0 && !kDiag<kDiagNoBeta>) {
             if (tl >= 1) {
                 // j = 0 (nothing) and j = 1 (window tl, maybe partial: the rolled loop), then the full
                 // windows wb = tl-1 .. 0 (j = 2 .. nB-2) with running slot counters
@@ -2179,13 +1603,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wb = tl - j + 1;
-#ifdef TD_DIAG_NOBETA   // diagnostics only (wrong results): the B pass without the beta chain
-            if (false)
-#else
-            if (wb >= 0 && wb <= tl)
-#endif
+            if (!kDiag<kDiagNoBeta> && wb >= 0 && wb <= tl)
                 beta = beta_window<T, ALGO>(beta, wb, window_len(gm, wb), sm, lut_col(sm, lane), lane >> 3, lc,
-                                                                        st ? st + 4 : nullptr);
+                                            st ? st + 4 : nullptr);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -2194,9 +1614,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     } else {
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
-        int fe = (wave == 0 ? 0 : kFoldA<ALGO>) + lane;
-        int nfold = wave == 0 ? kFoldA<ALGO> : kTile - kFoldA<ALGO>;
-        if constexpr (!kFoldRows<ALGO> && (ALGO == 0 || TD_ML_FOLD_MAP) && kTile - kTile / 3 <= kLanes) {
+        int fe = (wave == 0 ? 0 : kFoldA) + lane;
+        int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
+        if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
             // takes the 32 items of the phase furthest from a kept row (pd), the fold wave beside
@@ -2209,25 +1629,14 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
         }
         int j0 = 0;
-        if (TD_FOLD_FAST && (ALGO == 0 || kAvDirect || kArec) && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
+        if (ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
             // here iterations 3 .. nB-1, i.e. the full windows wf = tl-1 .. 0
-            // TD_AV_DIRECT: the lane's alpha block of window wf is loaded two iterations ahead
-            // (acur: this window, anext: the next), the first two before iteration 0
-            const int fk = min(fe >> 3, kW - 1);   // spare lanes: any valid row (they fold nothing)
-            int fks = fk;
-            if constexpr (!kFoldRows<ALGO>) ck_row_of<ALGO>(fk, fks);   // the stored row at or before fk
-            const T* ag = ga0 + (size_t)fks * arow + (fe & 7) * 8;
-            T acur[8], anext[8];
-            if constexpr (kAvDirect) {
-                load_block_global<T>(ag + (size_t)(tl - 1) * aws, acur);
-                load_block_global<T>(ag + (size_t)max(tl - 2, 0) * aws, anext);
-            }
             for (int j = 0; j < 3; ++j) {
                 TD_STAMP(b0);
                 const int wf = tl - j + 2;
                 if (lane < nfold && wf <= tl && (fe >> 3) < window_len(gm, wf))
-                    fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm, astore);
+                    fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
                 TD_STAMP(b1);
                 wg_sync_lds();
                 TD_STAMP(b2);
@@ -2235,20 +1644,18 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 TD_ACC(3, b1, b2);
             }
             FoldLane<T> fl;
-            const bool f1split = kFoldSplit<ALGO> && wave != 0;   // F1: one chain per lane (fold_item_split)
-            const int fes = f1split ? kFoldA<ALGO> + (lane & 31) : fe;
-            fl.k = fes >> 3;
-            fl.c = fes & 7;
+            fl.k = fe >> 3;
+            fl.c = fe & 7;
             const int ke = min(fl.k, kW - 1);   // spare lanes: any valid row (they fold nothing)
             fl.G = &sm.G[0][ke][fl.c][0];
             fl.Wp = &sm.Wp[0][ke][0];
             fl.Bv = &sm.Bv[0][ke][fl.c * 8];
             if constexpr (kFoldRows<ALGO>) {
-                fl.Av = &sm.Av[0][kAvDirect ? 0 : ke][fl.c * 8];
+                fl.Av = &sm.Av[0][ke][fl.c * 8];
             } else {
                 int ks;
                 const int r = ck_row_of<ALGO>(ke, ks);
-                fl.Av = &sm.Av[0][kAvDirect ? 0 : r][fl.c * 8];
+                fl.Av = &sm.Av[0][r][fl.c * 8];
                 fl.arot = av_rot<ALGO>(r, fl.c);
                 fl.rec = ke - ks;
                 fl.Gr = &sm.G[0][ks][fl.c][0];
@@ -2259,37 +1666,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
-            if constexpr (kFoldSplit<ALGO>) {
-                if (f1split) {   // F1, one chain per lane: its own loop (one instruction stream per role)
-                    const int u = lane >> 5;
-                    for (int j = 3; j < nB; ++j, --wf) {
-                        TD_STAMP(b0);
-                        fold_item_split<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K, u, true);
-                        s3 = s3 == 0 ? 2 : s3 - 1;
-                        s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
-                        s2 ^= 1;
-                        TD_STAMP(b1);
-                        wg_sync_lds();
-                        TD_STAMP(b2);
-                        TD_ACC(2, b0, b1);
-                        TD_ACC(3, b1, b2);
-                    }
-                }
-            }
-            for (int j = 3; j < nB && !(kFoldSplit<ALGO> && f1split); ++j, --wf) {
+            for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
-                T afar[8];
-                if constexpr (kAvDirect) load_block_global<T>(ag + (size_t)max(wf - 2, 0) * aws, afar);
-#ifndef TD_DIAG_NOFOLD
-                if (lane < nfold) fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K, acur);
-#endif
-                if constexpr (kAvDirect) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        acur[q] = anext[q];
-                        anext[q] = afar[q];
-                    }
-                }
+                if (!kDiag<kDiagNoFold> && lane < nfold)
+                    fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
                 s3 = s3 == 0 ? 2 : s3 - 1;
                 s4 = s4 == 0 ? kAvSlots - 1 : s4 - 1;
                 s2 ^= 1;
@@ -2304,10 +1684,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
-#ifndef TD_DIAG_NOFOLD   // diagnostics only: the B pass without its folds (wrong results)
-            if (lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
-                fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm, astore);
-#endif
+            if (!kDiag<kDiagNoFold> && lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
+                fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
             wg_sync_lds();
             TD_STAMP(b2);
@@ -2337,72 +1715,39 @@ __device__ __forceinline__ Smem<T>* smem()
 }
 
 // VALU issue priority of the beta wave (ties on a SIMD go to the higher priority, then the older
-// wave).  Log-MAP fp64: beta bounds the B pass, so it goes first (2).  fp32 log-MAP and Max-Log-MAP:
-// the folds bound the B pass and beta yields (0).  TD_BETA_PRIO_* override.
-#ifndef TD_BETA_PRIO_F64
-#define TD_BETA_PRIO_F64 2
-#endif
-#ifndef TD_BETA_PRIO_F32
-#define TD_BETA_PRIO_F32 2   // fp32 log-MAP: 0 measured best before its table went to 32 columns; now 2 (1414 -> 1436)
-#endif
-#ifndef TD_BETA_PRIO_MAXLOG
-#define TD_BETA_PRIO_MAXLOG 0
-#endif
+// wave).  Log-MAP: beta bounds the B pass, so it goes first (2; fp32 log-MAP measured best at 0
+// before its table went to 32 columns, 2 since: 1414 -> 1436).  Max-Log-MAP: the folds and the
+// loader bound the B pass and beta yields (0).
 template <typename T, int ALGO>
 __device__ __forceinline__ void set_beta_prio()
 {
-    if constexpr (ALGO == 1)
-        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_MAXLOG);
-    else if constexpr (sizeof(T) == 8)
-        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F64);
-    else
-        __builtin_amdgcn_s_setprio(TD_BETA_PRIO_F32);
+    __builtin_amdgcn_s_setprio(ALGO == 1 ? 0 : 2);
 }
 
 struct WgPos {
-    int group;   // codeword group within the workgroup
-    int role;    // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
+    int role;       // 0 = A, 1 = B (beta), 2 = F0 (loader), 3 = F1 (fold)
     int lane;
-    int g;       // global codeword group index
-    int slot_key;   // TD_ROLE_MAP 2: this CU's occupancy word, and the slot taken (4: none)
+    int g;          // codeword group index
+    int slot_key;   // this CU's occupancy word, and the slot taken (4: none)
     int slot;
 };
 
-// With one group per workgroup, two workgroups share a CU: blocks b and b + nCU (the second
-// dispatch round), whose wave w lands on the SIMD of the first one's wave w+1.  The second round
-// rotates its roles by 3 so that each recursion wave shares its SIMD with a light role of the other
-// workgroup: A with F0 (the loader), B with F1 (the fold wave, idle in the F pass) -- instead of
-// A with F1 and B with A.  role_cus = the CU count (0: no rotation).
-//
-// TD_ROLE_MAP 1 (measured slower, kept for diagnostics) pairs the roles per SIMD as
-//   S0: B + F0'   S1: F0 + B'   S2: A + F1'   S3: F1 + A'      (' = the second-round workgroup)
-// i.e. wave -> role {B, F0, A, F1} in the first round and {B, F1, A, F0} in the second: in the F
-// pass each alpha chain has its SIMD to itself (F1 idles there), and in the B pass each beta chain
-// shares only with a loader, the two fold waves sharing the remaining SIMDs.
-//
-// TD_ROLE_MAP 2 (default) makes the pairing independent of the dispatcher: the waves read their
-// SIMD from HW_ID and the workgroup takes a free slot (0 or 1; 2 for turbo_decode_kernel3) of its CU in a per-CU occupancy
-// word (atomicOr; released at the end, wg_release); role = SIMD for slot 0 and SIMD ^ 2 for slot
-// 1, which gives the pairs A/F0, B/F1 on every SIMD whatever order the workgroups arrived in
-// (a preceding kernel with many small blocks shifted the round-based placement: +4 % kernel time).
-// If two waves of the workgroup share a SIMD, the wave index stands in for the SIMD.
-#ifndef TD_ROLE_MAP
-#define TD_ROLE_MAP 2
-#endif
-#ifndef TD_SLOT_XOR
-#define TD_SLOT_XOR 2   // map 2: the second workgroup's role on a SIMD = first's ^ 2 (A/F0, B/F1); 3: A/F1, B/F0
-#endif
+// Roles by placement.  Two workgroups share a CU (three or four in turbo_decode_kernel3 / 4), and a
+// recursion wave should share its SIMD with a light role of the other workgroup: A with F0 (the
+// loader), B with F1 (the fold wave, idle in the F pass).  The waves read their SIMD from HW_ID and
+// the workgroup takes a free slot (0..3) of its CU in a per-CU occupancy word (atomicOr; released at
+// the end, wg_release); role = SIMD for slot 0 and SIMD ^ 2 for slot 1, which gives the pairs A/F0,
+// B/F1 on every SIMD whatever order the workgroups arrived in (deriving the pairing from the
+// dispatch round instead cost 4 % after a kernel with many small blocks had shifted the placement;
+// the pairing A/F1 + B/F0 measured 0.7 % slower, and beta beside a loader -- alpha alone on its SIMD
+// in the F pass -- 1.3 % slower).  If two waves of the workgroup share a SIMD, the wave index stands
+// in for the SIMD.  role_cus = 0 or no slot words (diagnostics, TD_ROLE_ROT=0): role = wave.
 __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = kGroupsPerWg > 1 ? wave >> 2 : 0;
     const int lane = (int)(threadIdx.x & 63);
-    const int g = (int)blockIdx.x * kGroupsPerWg + h;
-    // TD_AREC: waves 0, 1, 2, 3, 4 -> A, B, R, F1, F0 (roles 0, 1, 4, 3, 2): with waves w and w+4 on
-    // one SIMD the two B-pass chains (B, R) each have a SIMD of their own within the workgroup,
-    // and A shares its SIMD with the loader (as TD_ROLE_MAP 2 pairs them)
-    if (kWaves == 5) return WgPos{h, TD_AREC_ROLES ? (wave == 2 ? 4 : (wave == 4 ? 2 : wave)) : wave, lane, g, 0, 4};
-    if (TD_ROLE_MAP == 2 && kGroupsPerWg == 1 && role_cus > 0 && slots) {
+    const int g = (int)blockIdx.x;
+    if (role_cus > 0 && slots) {
         __shared__ int s_simd[kWaves];
         __shared__ int s_slot;
         const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
@@ -2425,19 +1770,10 @@ __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
         const int base = distinct ? simd : wave;
         // slots 2, 3 (turbo_decode_kernel3 / 4): role = SIMD ^ 1, SIMD ^ 3, so that the workgroups'
         // alpha chains (and their beta chains) sit on different SIMDs
-        const int rx = slot == 1 ? TD_SLOT_XOR : (slot == 2 ? 1 : (slot == 3 ? 3 : 0));
-        return WgPos{h, base ^ rx, lane, g, key, slot};
+        const int rx = slot == 1 ? 2 : (slot == 2 ? 1 : (slot == 3 ? 3 : 0));
+        return WgPos{base ^ rx, lane, g, key, slot};
     }
-    const bool second = kGroupsPerWg == 1 && role_cus > 0 && ((int)blockIdx.x / role_cus) % 2;
-    int role;
-    if (TD_ROLE_MAP == 1 && kGroupsPerWg == 1) {
-        constexpr unsigned first_map = 1u | (2u << 2) | (0u << 4) | (3u << 6);    // B F0 A F1
-        constexpr unsigned second_map = 1u | (3u << 2) | (0u << 4) | (2u << 6);   // B F1 A F0
-        role = (int)(((second ? second_map : first_map) >> (2 * (wave & 3))) & 3u);
-    } else {
-        role = ((wave & 3) ^ (h ? TD_ROLE_XOR : 0)) + (second ? 3 : 0) & 3;
-    }
-    return WgPos{h, role, lane, g, 0, 4};   // slot 4: none (wg_release)
+    return WgPos{wave, lane, g, 0, 4};   // slot 4: none (wg_release)
 }
 
 // end of the kernel: give the CU slot back (all waves of the workgroup are past their work)
@@ -2454,7 +1790,7 @@ template <typename T, int ALGO>
 __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
 {
     const WgPos w = wg_pos(p.role_cus, p.cu_slots);
-    Smem<T>& sm = smem<T>()[w.group];
+    Smem<T>& sm = *smem<T>();
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
     if (wave == 1) set_beta_prio<T, ALGO>();   // beta first; alpha raises itself in the F pass
@@ -2500,45 +1836,36 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
 }
 
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void turbo_decode_kernel(DecodeParams<T> p)
+__global__ __launch_bounds__(kWaves * 64, 2) void turbo_decode_kernel(DecodeParams<T> p)
 {
     turbo_decode_body<T, ALGO>(p);
 }
 
 // Large batches (more groups than two per CU): three workgroups per CU -- 24 codewords, 12 waves,
 // three per SIMD -- where the build fits them: at most 168 VGPRs without scratch (the build fails
-// on scratch) and a third of the CU's LDS.  fp32 Max-Log-MAP fits as it is (143 VGPRs, 42 KB); the
-// other modes need TD_ROLE_REMAT (fp32 log-MAP 191 -> 78 VGPRs, fp64 240-256 -> 95-106) and fp64
-// also TD_AV_DIRECT (69.9 -> 45.8 KB of LDS).  Measured (B = 12288, one box): fp32 Max-Log-MAP 2370
-// -> 3357 Mbit/s, fp32 log-MAP 1641 -> 2265; fp64 with TD_AV_DIRECT=1 and TD_ROLE_REMAT=2 gained
-// 2-9 % at 12288 and nothing at 32768 (HBM-bound) and lost 9 % at B = 4096, so fp64 stays on two.
-#ifndef TD_OCC3
-#define TD_OCC3 1
-#endif
+// on scratch) and a third of the CU's LDS.  fp32 fits (role remat: fp32 log-MAP 191 -> 78 VGPRs).
+// fp64 does not: its Smem (the 4-window alpha ring alone is 30 KB) is more than a third of the CU's
+// LDS.  Measured (B = 12288, one box): fp32 Max-Log-MAP 2370 -> 3357 Mbit/s, fp32
+// log-MAP 1641 -> 2265.
 template <typename T, int ALGO>
-constexpr bool kOcc3 = TD_OCC3 != 0 && kGroupsPerWg == 1 && 3 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
-                       (kRoleRemat<T> || (sizeof(T) == 4 && ALGO == 1));
+constexpr bool kOcc3 = 3 * (sizeof(Smem<T>) + 64) <= 160 * 1024 && (kRoleRemat<T> || (sizeof(T) == 4 && ALGO == 1));
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kWaves * 64, kArec ? 4 : 3) void turbo_decode_kernel3(DecodeParams<T> p)
+__global__ __launch_bounds__(kWaves * 64, 3) void turbo_decode_kernel3(DecodeParams<T> p)
 {
     if constexpr (kOcc3<T, ALGO>) turbo_decode_body<T, ALGO>(p);
 }
 
 // More than three groups per CU: four workgroups per CU (16 waves, at most 128 VGPRs, a quarter of
-// the LDS) where they fit: fp32 (36.7 KB of LDS, 67-79 VGPRs with TD_ROLE_REMAT).
-#ifndef TD_OCC4
-#define TD_OCC4 1
-#endif
+// the LDS) where they fit: fp32 with 12-step windows (36.7 KB of LDS, 67-79 VGPRs with role remat).
 template <typename T, int ALGO>
-constexpr bool kOcc4 = TD_OCC4 != 0 && !kArec && kGroupsPerWg == 1 && 4 * (sizeof(Smem<T>) + 64) <= 160 * 1024 &&
-                       kRoleRemat<T>;
+constexpr bool kOcc4 = 4 * (sizeof(Smem<T>) + 64) <= 160 * 1024 && kRoleRemat<T>;
 // fp32 four per CU from the 12-step-window build when this one's Smem does not fit four (launch_turbo4_w12)
 #ifdef TD_W12_TU
 template <typename T, int ALGO>
 constexpr bool kOcc4W12 = false;
 #else
 template <typename T, int ALGO>
-constexpr bool kOcc4W12 = TD_OCC4 != 0 && !kOcc4<T, ALGO> && sizeof(T) == 4 && kW != 12 && !kArec && kGroupsPerWg == 1;
+constexpr bool kOcc4W12 = !kOcc4<T, ALGO> && sizeof(T) == 4 && kW != 12;
 #endif
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kWaves * 64, 4) void turbo_decode_kernel4(DecodeParams<T> p)
@@ -2550,7 +1877,7 @@ __global__ __launch_bounds__(kWaves * 64, 4) void turbo_decode_kernel4(DecodePar
 // turbo_decode_kernel under its own symbol, so that kernel traces and PMC passes of a decode list
 // the one-iteration probe launches apart from the decode's own launches.
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void turbo_placement_probe_kernel(
+__global__ __launch_bounds__(kWaves * 64, 2) void turbo_placement_probe_kernel(
     DecodeParams<T> p)
 {
     turbo_decode_body<T, ALGO>(p);
@@ -2558,11 +1885,11 @@ __global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroups
 
 // Standalone SISO (Log_MAP_decoder) over interleaved [G][L][8] inputs.
 template <typename T, int ALGO>
-__global__ __launch_bounds__(kGroupsPerWg * kWaves * 64, kArec ? 3 : 2 / kGroupsPerWg) void siso_kernel(DecodeParams<T> p, const T* la,
+__global__ __launch_bounds__(kWaves * 64, 2) void siso_kernel(DecodeParams<T> p, const T* la,
                                                                                           int terminated)
 {
     const WgPos w = wg_pos(p.role_cus, p.cu_slots);
-    Smem<T>& sm = smem<T>()[w.group];
+    Smem<T>& sm = *smem<T>();
     const int wave = w.role, lane = w.lane;
     lut_to_lds(p, sm, wave * kLanes + lane);
     if (wave == 1) set_beta_prio<T, ALGO>();
@@ -2708,11 +2035,10 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
     for (int j = 0; j < 8; ++j) v[j] = (j == 0 || !slot0_only) ? x0 : (T)-kInfty;
 }
 
-#ifndef TD_SW_WAVES
-#define TD_SW_WAVES 1   // minimum waves per SIMD asked of the register allocator (1: no limit)
-#endif
+// (Four waves per SIMD asked of the register allocator measured 7 % slower in fp64 and +1 % with
+// scratch in fp32: not kept.)
 template <typename T, int ALGO, int S>
-__global__ __launch_bounds__(256, TD_SW_WAVES) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
+__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[kLutElems<T>];
     if constexpr (ALGO == 0) {
@@ -2834,16 +2160,12 @@ __global__ __launch_bounds__(256, TD_SW_WAVES) void sw_siso_kernel(DecodeParams<
     }
 }
 
-#ifndef TD_SW_SEG_F64
-#define TD_SW_SEG_F64 4   // 2 (4 waves/SIMD, half the recompute, twice the checkpoint traffic) measured -12 %
-#endif
-#ifndef TD_SW_SEG_F32
-#define TD_SW_SEG_F32 8
-#endif
+// checkpoint spacing S: the segment's alpha stays in registers.  fp64: 4 (2 -- 4 waves/SIMD, half the
+// recompute, twice the checkpoint traffic -- measured -12 %; 3 and 5 -6 %); fp32: 8.
 template <typename T>
 constexpr int sw_seg()
 {
-    return sizeof(T) == 4 ? TD_SW_SEG_F32 : TD_SW_SEG_F64;   // checkpoint spacing S: the segment's alpha stays in registers
+    return sizeof(T) == 4 ? 8 : 4;
 }
 
 template <typename T, int ALGO>
@@ -2905,19 +2227,7 @@ hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const 
     return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st) : launch_window_algo<T, 0>(p, w, wb, st);
 }
 
-#ifndef TD_DEMUX_PERM
-#define TD_DEMUX_PERM 1
-#endif
-#ifndef TD_DEMUX_BLOCKS
-#define TD_DEMUX_BLOCKS 32768   // grid cap of demux_kernel (grid-stride loop beyond); 8192: 0.230 ms, 32768: 0.212 (config 2)
-#endif
-constexpr bool kDemuxPerm = TD_DEMUX_PERM != 0;   // 0: sys2 gathered from the stream in demux_kernel
-#ifndef TD_PERM_XCD
-#define TD_PERM_XCD 1
-#endif
-#ifndef TD_PERM_NT
-#define TD_PERM_NT 0
-#endif
+constexpr int kDemuxBlocks = 32768;   // grid cap of demux_kernel (grid-stride loop beyond); 8192: 0.230 ms, 32768: 0.212 (config 2)
 
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
 // batch-interleaved arrays, in two passes:
@@ -2947,7 +2257,6 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
                 ys1 = r[3 * i] * h;
                 yp1 = r[3 * i + 1] * h;
                 yp2 = r[3 * i + 2] * h;
-                if (!kDemuxPerm) p.sys2[e] = r[3 * p.pi[i]] * h;
             } else {
                 const int j = i - K;
                 ys1 = r[3 * K + 2 * j] * h;
@@ -2955,7 +2264,7 @@ __global__ __launch_bounds__(256) void demux_kernel(DecodeParams<T> p, const T* 
                 p.sys2[e] = r[3 * K + 2 * kMemory + 2 * j] * h;
                 yp2 = r[3 * K + 2 * kMemory + 2 * j + 1] * h;
             }
-        } else if (i >= K || !kDemuxPerm) {
+        } else if (i >= K) {
             p.sys2[e] = 0;
         }
         p.sys1[e] = ys1;
@@ -2969,22 +2278,13 @@ template <typename T>
 __global__ __launch_bounds__(kPermBlock) void demux_perm_kernel(DecodeParams<T> p, int blocks_per_group)
 {
     const int b = blockIdx.x;
-#if TD_PERM_XCD
     const int xcd = b % 8, r = b / 8;                              // XCD-major: group g on XCD g % 8
     const int g = (r / blocks_per_group) * 8 + xcd;
     const int e = (r % blocks_per_group) * kPermBlock + (int)threadIdx.x;   // (step, codeword) in the group
-#else
-    const int g = b / blocks_per_group;
-    const int e = (b % blocks_per_group) * kPermBlock + (int)threadIdx.x;
-#endif
     if (g >= p.G || e >= p.K * kCw) return;
     const int i = e >> 3, c = e & 7;
     const size_t row = (size_t)g * p.L;
-#if TD_PERM_NT
-    __builtin_nontemporal_store(p.sys1[(row + p.pi[i]) * kCw + c], &p.sys2[(row + i) * kCw + c]);
-#else
     p.sys2[(row + i) * kCw + c] = p.sys1[(row + p.pi[i]) * kCw + c];
-#endif
 }
 
 // Bare-SISO input transpose: recs[B][2L] / La[B][L] -> [G][L][8]
@@ -3050,9 +2350,9 @@ constexpr size_t kMinWgLds = 160 * 1024 / 3 + 1024;
 template <typename T>
 constexpr size_t wg_lds()
 {
-    return kGroupsPerWg * sizeof(Smem<T>) > kMinWgLds ? kGroupsPerWg * sizeof(Smem<T>) : kMinWgLds;
+    return sizeof(Smem<T>) > kMinWgLds ? sizeof(Smem<T>) : kMinWgLds;
 }
-static_assert(kGroupsPerWg != 1 || 2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
+static_assert(2 * (sizeof(Smem<double>) + 64) <= 160 * 1024, "two workgroups per CU");
 
 
 // turbo_decode_kernel3's LDS: never less than a quarter of the CU's plus 1 KB, so that at most three
@@ -3117,11 +2417,9 @@ hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool prob
     hipError_t e = allow_smem(k, wg_lds<T>());
     if (e != hipSuccess) return e;
     if (probe)
-        hipLaunchKernelGGL((turbo_placement_probe_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg),
-                           dim3(kGroupsPerWg * kWaves * kLanes), wg_lds<T>(), st, p);
+        hipLaunchKernelGGL((turbo_placement_probe_kernel<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), wg_lds<T>(), st, p);
     else
-        hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg),
-                           dim3(kGroupsPerWg * kWaves * kLanes), wg_lds<T>(), st, p);
+        hipLaunchKernelGGL((turbo_decode_kernel<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), wg_lds<T>(), st, p);
     return hipGetLastError();
 }
 
@@ -3130,8 +2428,7 @@ hipError_t launch_siso_algo(const DecodeParams<T>& p, const T* la, int terminate
 {
     hipError_t e = allow_smem(reinterpret_cast<const void*>(&siso_kernel<T, ALGO>), wg_lds<T>());
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((siso_kernel<T, ALGO>), dim3(p.G / kGroupsPerWg), dim3(kGroupsPerWg * kWaves * kLanes),
-                       wg_lds<T>(), st, p, la, terminated);
+    hipLaunchKernelGGL((siso_kernel<T, ALGO>), dim3(p.G), dim3(kWaves * kLanes), wg_lds<T>(), st, p, la, terminated);
     return hipGetLastError();
 }
 
@@ -3140,11 +2437,11 @@ hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
 {
     const size_t total = (size_t)p.G * p.L * kCw;
     int gblocks = (int)((total + 255) / 256);
-    if (gblocks > TD_DEMUX_BLOCKS) gblocks = TD_DEMUX_BLOCKS;
+    if (gblocks > kDemuxBlocks) gblocks = kDemuxBlocks;
     hipLaunchKernelGGL(demux_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, flow);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (!kDemuxPerm || p.sys2_in_turbo) return hipSuccess;
+    if (p.sys2_in_turbo) return hipSuccess;
     const int bpg = (p.K * kCw + kPermBlock - 1) / kPermBlock;
     const long long pblocks = (long long)((p.G + 7) / 8) * 8 * bpg;
     hipLaunchKernelGGL(demux_perm_kernel<T>, dim3((unsigned)pblocks), dim3(kPermBlock), 0, st, p, bpg);
@@ -3163,7 +2460,7 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 {
     const size_t total = (size_t)p.G * p.L * kCw;
     int gblocks = (int)((total + 255) / 256);
-    if (gblocks > TD_DEMUX_BLOCKS) gblocks = TD_DEMUX_BLOCKS;
+    if (gblocks > kDemuxBlocks) gblocks = kDemuxBlocks;
     hipLaunchKernelGGL(siso_in_kernel<T>, dim3(gblocks), dim3(256), 0, st, p, recs, la, la_ws);
     hipError_t e = p.algo == 1 ? launch_siso_algo<T, 1>(p, la_ws, terminated, st)
                                : launch_siso_algo<T, 0>(p, la_ws, terminated, st);
@@ -3187,8 +2484,6 @@ template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*,
                                        hipStream_t);
 
 int window_steps() { return kW; }
-static_assert(kW == kWindowSteps, "td_kernels.h kWindowSteps is the kernel's window");
-int groups_per_wg() { return kGroupsPerWg; }
 #endif
 
 }  // namespace td / td_w12
