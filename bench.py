@@ -20,6 +20,9 @@ Extra objects on the JSON line:
                 `traffic` from the committed rocprofv3 PMC profile of the same config (or null)
   cpu_baseline  the compiled reference (oracle/_ref/ref_harness: ITTC/log_map.cpp's SISO and loop) on the
                 host cores, rank 0, N=1; the C restatement (oracle/) where that binary is absent
+  dropin        what the unchanged ITTC/main.cpp caller gets: TurboDecoding one frame per call through
+                libturbo_logmap_compat.so (examples/dropin_latency.cpp, 15 iterations = N_ITERATION),
+                next to the compiled reference's own per-frame time on one host core
   variants      fp32 log-MAP, fp64/fp32 Max-Log-MAP on the same batch; BASELINE config 5 (sliding
                 window 64, overlap 30) at its own batch of 32768 (fewer steps)
 """
@@ -69,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--window", type=int, default=0, help="0 = exact schedule; 64 = sliding window (config 5)")
     ap.add_argument("--overlap", type=int, default=30, help="sliding-window warm-up steps")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--dropin-frames", type=int, default=8,
+                    help="frames for the drop-in per-frame latency (0 = skip; N=1, fp64 log-MAP only)")
     return ap.parse_args(argv)
 
 
@@ -97,6 +102,12 @@ def qpp_for(K):
     if K == 40:
         return 3, 10
     raise SystemExit("bench: give K in {40, 1024, 6144}")
+
+
+def window_steps() -> int:
+    """Steps per window of the loaded library's exact-schedule kernel (td_window_steps)."""
+    from turbo_decoder_cuda_amd import _native as N
+    return int(N.lib().td_window_steps())
 
 
 def load_traffic(cfg_key):
@@ -164,6 +175,12 @@ def main():
     barrier()
     demux_ms, turbo_ms, nlaunch = codec.kernel_ms()
     codec.profile(False)
+    clock = None
+    if not a.window:   # the last launch's sustained shader clock (td_clock_read), outside the timed region
+        try:
+            clock = codec.clock()
+        except Exception:
+            clock = None
 
     errs = int((bits != u_d).sum().item())
     blk = int((bits != u_d).any(dim=1).sum().item())
@@ -171,15 +188,16 @@ def main():
         os.makedirs(a.dump_bits, exist_ok=True)
         np.save(os.path.join(a.dump_bits, f"bits_rank{rank}_first{first}.npy"), bits.cpu().numpy())
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
-    out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
-    out["workspace_placement"] = {"probe_ms": placement[0], "kept": placement[1],
-                                  "note": "one-iteration probe per candidate workspace at td_reserve (outside the timed region)"}
+    out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock)
+    out["workspace_placement"] = placement_record(placement, turbo_ms, a.iters)
 
     if rank == 0 and world == 1 and not a.no_variants:
         out["pcie_inclusive"] = pcie_inclusive(a, codec, llr, dev, stream)
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         n = min(a.cpu_sample, a.batch)
         out["cpu_baseline"] = cpu_baseline(a, llr64[:n].cpu().numpy(), bits[:n].cpu().numpy(), f1, f2)
+    if rank == 0 and world == 1 and a.dropin_frames > 0 and not a.window and a.precision == "f64" and a.algo == "logmap":
+        out["dropin"] = dropin(a, llr64[: a.dropin_frames].cpu().numpy(), f1, f2, local)
     if rank == 0 and world == 1 and not a.no_variants:
         out["variants"] = variants(a, codec, llr64, u_d, f1, f2, dev, stream)
         out["demod"] = demod_rates(a, dev)
@@ -187,6 +205,67 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def placement_record(placement, turbo_ms: float, iters: int) -> dict:
+    """td_reserve's workspace placement search beside the full launch it chose for: the kept
+    candidate's one-iteration probe time x iterations is what the probe predicts for a launch, so a
+    'fast probe, slow launch' box shows as launch_over_probe well above 1."""
+    ms, kept = placement
+    rec = {"probe_ms": ms, "kept": kept,
+           "note": "one-iteration probe per candidate workspace at td_reserve (outside the timed region)"}
+    if ms and 0 <= kept < len(ms):
+        rec["kept_probe_ms"] = ms[kept]
+        rec["probe_x_iters_ms"] = round(ms[kept] * iters, 4)
+        rec["launch_ms"] = round(turbo_ms, 4)
+        rec["launch_over_probe"] = round(turbo_ms / (ms[kept] * iters), 4) if ms[kept] > 0 else None
+    return rec
+
+
+DROPIN = os.path.join(REPO, "turbo_decoder_cuda_amd", "td_dropin_latency")
+
+
+def dropin(a, flows, f1, f2, device: int) -> dict:
+    """The unchanged reference caller's per-frame latency (ITTC/main.cpp:221: one TurboDecoding per
+    frame, 15 iterations = N_ITERATION): examples/dropin_latency.cpp linked against
+    libturbo_logmap_compat.so, a child process on this GPU, warm handle after its first frame.  Beside
+    it the compiled reference's TurboDecoding loop on one host core at 15 iterations, per frame.
+    Bits: the drop-in's last-iteration rows against the reference's on the same frames."""
+    import subprocess
+    import tempfile
+
+    n = flows.shape[0]
+    rec = {"frames": n, "iterations": 15, "K": a.K, "caller": "ITTC/main.cpp:221 TurboDecoding(flow, out, 3K+12)"}
+    if not os.access(DROPIN, os.X_OK):
+        rec["error"] = "td_dropin_latency not built"
+        return rec
+    env = dict(os.environ, TD_ITERATIONS="15", TD_DEVICE=str(device))
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "flows.bin"), os.path.join(td, "bits.bin")
+        np.ascontiguousarray(flows, dtype=np.float64).tofile(fin)
+        r = subprocess.run([DROPIN, str(a.K), str(f1), str(f2), str(n), fin, fout], capture_output=True, text=True,
+                           env=env, timeout=300)
+        if r.returncode:
+            rec["error"] = (r.stdout + r.stderr)[-400:]
+            return rec
+        rec.update(json.loads(r.stdout.strip().splitlines()[-1]))
+        gpu_bits = np.fromfile(fout, dtype=np.uint8).reshape(n, a.K)
+        if os.access(REF_HARNESS, os.X_OK):
+            nr = min(n, 4)
+            rout = os.path.join(td, "rbits.bin")
+            np.ascontiguousarray(flows[:nr], dtype=np.float64).tofile(fin)
+            rr = subprocess.run([REF_HARNESS, "decode", str(a.K), str(f1), str(f2), "15", "1", fin, rout],
+                                capture_output=True, text=True, check=True, timeout=600)
+            dt = float(rr.stdout.split()[1])
+            ref_bits = np.fromfile(rout, dtype=np.uint8).reshape(nr, a.K)
+            rec["reference_ms_per_frame"] = round(dt / nr * 1e3, 3)
+            rec["reference"] = f"the compiled reference (ITTC/log_map.cpp, g++ -O2), one host core, {nr} frames"
+            rec["bits_match_reference"] = bool(np.array_equal(gpu_bits[:nr], ref_bits))
+            rec["speedup_vs_reference"] = round(rec["reference_ms_per_frame"] / rec["ms_per_frame"], 3)
+    rec["note"] = ("per-frame latency of the batch-of-one path: one codeword group on one CU, so the time is "
+                   "the serial alpha / beta chains of 30 SISOs (DESIGN.md 5); throughput callers batch "
+                   "(td_decode_device), the headline value")
+    return rec
 
 
 def reduce_over_ranks(elapsed: float, errs: int, blk: int, world: int):
@@ -204,25 +283,38 @@ def reduce_over_ranks(elapsed: float, errs: int, blk: int, world: int):
     return float(t.item()), int(e[0]), int(e[1])
 
 
-def traffic_model(K: int, B: int, iters: int, esz: int, algo: str) -> dict:
+def traffic_model(K: int, B: int, iters: int, esz: int, algo: str, W: int = 15, alpha_raw: bool = True) -> dict:
     """HBM bytes per turbo-kernel launch by stream, from the exact schedule's access pattern
-    (groups G = ceil(B/8), L = K+3, nT = ceil(L/12) windows, 2*iters SISOs):
-      alpha     F pass writes one 64-element row per step (log-MAP; Max-Log-MAP one in three), the
-                B pass DMAs whole 12-row windows back (log_map.cpp:975-1001 alpha, kept for the LLRs)
-      tempmax   one 8-element row per step written, whole windows read back (beta's :1019 input)
-      inputs    ys, yp, La tiles (+ write positions) staged once in the F pass, again in the B pass
+    (groups G = ceil(B/8), L = K+3, windows of W steps (td_window_steps()),
+    nT = ceil(L/W), 2*iters SISOs):
+      alpha     log-MAP: the F pass writes alpha_raw, one 64-element row per step and row L; the B
+                pass DMAs whole W-row windows back, plus the first DMA of the window after the last
+                (log_map.cpp:975-1001 alpha, kept for the LLRs; beta's tempmax is the max of the rows).
+                Max-Log-MAP: one row in three written, W/3 rows a window read back
+      tempmax   Max-Log-MAP only: one 8-element row per step written, whole windows read back (beta's
+                :1019 input); log-MAP forms it from the alpha rows on chip (round 4)
+      inputs    ys, yp, La tiles (+ the window's write positions) staged once in the F pass, again in
+                the B pass
       extrinsic Le written once per SISO (8 B per element, coalesced over a group's 8 codewords)
       sys2      the first SISO forms decoder 2's systematic input (a gather within L2, one write)
-    The sum is checked against the PMC total (FETCH_SIZE x2 + WRITE_SIZE) in profiles/traffic.json."""
+    alpha_raw=False models the round-3 (v29) log-MAP kernel: normalised alpha of L rows and the tempmax
+    stream.  The sum is checked against the PMC total (FETCH_SIZE x2 + WRITE_SIZE) in profiles/traffic.json."""
     G = (B + 7) // 8
     L = K + 3
-    nT = (L + 11) // 12
+    nT = (L + W - 1) // W
     S = 2 * iters
-    rows_a = L if algo == "logmap" else (L + 2) // 3
-    rows_a_read = nT * 12 if algo == "logmap" else nT * 4
-    alpha = S * G * (rows_a + rows_a_read) * 64 * esz
-    tm = S * G * (L + nT * 12) * 8 * esz
-    tile = 3 * 12 * 8 * esz + 2 * 12 * 4   # ys, yp, La rows + the window's write positions
+    row = 64 * esz
+    if algo == "logmap" and alpha_raw:
+        alpha = S * G * ((L + 1) * row + nT * W * row + 1024)
+        tm = 0
+    elif algo == "logmap":
+        alpha = S * G * (L + nT * W) * row
+        tm = S * G * (L + nT * W) * 8 * esz
+    else:
+        alpha = S * G * ((L + 2) // 3 + nT * (W // 3)) * row
+        tm = S * G * (L + nT * W) * 8 * esz
+    wp_chunks = W // 4 if W % 4 == 0 else (W + 6) // 4   # td_kernels.hip kWpChunks
+    tile = 3 * W * 8 * esz + 2 * wp_chunks * 16   # ys, yp, La rows + the window's write positions
     inputs = S * G * 2 * nT * tile
     ext = S * G * K * 8 * esz
     sys2 = G * K * 8 * esz * 2
@@ -230,33 +322,37 @@ def traffic_model(K: int, B: int, iters: int, esz: int, algo: str) -> dict:
     parts = {"alpha": alpha, "tempmax": tm, "inputs": inputs, "extrinsic": ext, "sys2": sys2, "bits": bits}
     total = sum(parts.values())
     return {"bytes": parts, "total": total, "share": {k: round(v / total, 4) for k, v in parts.items()},
-            "scratch_share": round((alpha + tm) / total, 4)}
+            "scratch_share": round((alpha + tm) / total, 4), "window_steps": W}
 
 
 # Dependent-chain cycles per trellis step of the two recursions, each alone on a SIMD with its
 # operands in registers (scripts/ubench_alpha.hip, scripts/ubench_beta.hip): fp64
 # log-MAP alpha 200 (218 with its two scratch stores), beta 148.
 CHAIN_CYCLES_F64_LOGMAP = {"alpha": 218, "beta": 148}
-SCLK_GHZ = 2.35   # the kernel's sustained shader clock on MI355X (s_memtime vs s_memrealtime)
+SCLK_GHZ = 2.35   # fallback only: the sustained shader clock measured on earlier boxes
 
 
-def latency_floor(a, turbo_ms):
+def latency_floor(a, turbo_ms, sclk_ghz=None):
     """The exact schedule's own speed of light: every codeword of a dispatch round is in flight at
     once, so a launch cannot beat 2*iters SISOs x L steps x (alpha step + beta step), the two serial
-    recursions back to back, at the chains' isolated per-step latency.  frac = floor / measured."""
+    recursions back to back, at the chains' isolated per-step latency, at the launch's own measured
+    shader clock (td_clock_read).  frac = floor / measured."""
     if a.window or a.algo != "logmap" or a.precision != "f64" or turbo_ms <= 0:
         return None
+    clk = sclk_ghz if sclk_ghz else SCLK_GHZ
     rounds = -(-((a.batch + 7) // 8) // 512)   # dispatch rounds of 512 workgroups (2 per CU)
     cyc = CHAIN_CYCLES_F64_LOGMAP["alpha"] + CHAIN_CYCLES_F64_LOGMAP["beta"]
-    floor_ms = rounds * 2 * a.iters * (a.K + 3) * cyc / (SCLK_GHZ * 1e9) * 1e3
+    floor_ms = rounds * 2 * a.iters * (a.K + 3) * cyc / (clk * 1e9) * 1e3
     return {"floor_ms": round(floor_ms, 3), "frac": round(floor_ms / turbo_ms, 4),
-            "chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP, "sclk_ghz": SCLK_GHZ, "dispatch_rounds": rounds,
+            "chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP, "sclk_ghz": round(clk, 4),
+            "sclk_source": "measured (td_clock_read)" if sclk_ghz else "constant (no clock sample)",
+            "dispatch_rounds": rounds,
             "note": "serial alpha + beta chains at their isolated per-step latency (microbenchmarks), "
                     "the bound this latency-limited kernel is measured against; the HBM fraction above "
                     "is the metric's contract"}
 
 
-def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2) -> dict:
+def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock=None) -> dict:
     """The bench JSON record.  value = info bits decoded by ALL ranks / max-over-ranks time."""
     ms_step = elapsed / a.steps * 1e3
     total = getattr(a, "total", a.batch * world)   # codewords of all ranks per step
@@ -268,7 +364,8 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
     achieved = alg_bytes / (turbo_ms * 1e-3) / 1e9 if turbo_ms > 0 else 0.0
     cfg_key = f"K{a.K}_B{a.batch}_it{a.iters}_{a.precision}_{a.algo}" + (f"_w{a.window}g{a.overlap}" if a.window else "")
     traffic = load_traffic(cfg_key)
-    model = None if a.window else traffic_model(a.K, a.batch, a.iters, esz, a.algo)
+    model = None if a.window else traffic_model(a.K, a.batch, a.iters, esz, a.algo, window_steps())
+    sclk = clock[0] if clock else None
     # measured HBM bytes (PMC) per launch over the live kernel time: what the memory system
     # actually moves (the exact kernel streams alpha / tempmax through HBM by design)
     traffic_gbs = traffic / (turbo_ms * 1e-3) / 1e9 if (traffic and turbo_ms > 0) else None
@@ -326,7 +423,9 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2)
             "traffic_frac_measured_ceiling": round(traffic_gbs / HBM_MEASURED_GBS, 4) if traffic_gbs else None,
             "measured_ceiling_gbs": HBM_MEASURED_GBS,
             "traffic_model": model,
-            "latency_floor": latency_floor(a, turbo_ms),
+            "latency_floor": latency_floor(a, turbo_ms, sclk),
+            "sclk_ghz": round(sclk, 4) if sclk else None,
+            "clock_span_ms": round(clock[1], 4) if clock else None,
             "limiter": ("latency of the serial alpha / beta recursions (one dependent trellis step at a time "
                         "per codeword; DESIGN.md 3.2): neither HBM nor VALU is saturated") if not a.window else
                        "VALU / LDS issue of the sub-block chains (DESIGN.md 8.3)",

@@ -129,6 +129,11 @@ int td_set_window(td_handle* h, const td_window_params* w);
  * `launches` decodes since the last read/enable, and starts a new accumulation. */
 int td_profile_enable(td_handle* h, int on);
 int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches);
+/* Launch clock (measurement support): every exact-schedule turbo launch records, in its first
+ * workgroup, the shader clock (s_memtime) and the 100 MHz real-time counter (s_memrealtime) at that
+ * workgroup's start and end.  td_clock_read synchronises the device and returns the last launch's
+ * sustained shader clock (GHz) and the workgroup's span (ms); TD_EINVAL before any such launch. */
+int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms);
 
 /* Diagnostics: in a library built with -DTD_STAMPS (td_debug_stamp_slots() > 0) the turbo
  * kernel writes per-wave shader-clock totals of its phases into d_buf [ceil(B/8)][slots]
@@ -143,7 +148,13 @@ int td_debug_placement(td_handle* h, float* ms, int cap, int* pick);
  * would stop after them (the fast mode seen), else 0; TD_EINVAL on a bad argument. */
 int td_debug_placement_rule(const float* ms, int n);
 
-/* Host-pointer convenience (pageable buffers; allocates, copies, decodes, synchronises).
+/* Trellis steps per window of the exact schedule's turbo kernel (15; fp32 at four workgroups per
+ * CU runs a 12-step build).  Measurement support: bench.py's traffic model. */
+int td_window_steps(void);
+
+/* Host-pointer convenience (pageable buffers; copies, decodes, synchronises).  The device staging
+ * buffers are the handle's, allocated on the first call and grown when B grows, so the per-frame
+ * caller (the drop-in's TurboDecoding) allocates nothing after its first frame.
  *   out  int[B][iterations][K] exactly like the reference's flow_decoded (one row per iteration)
  *   le   nullable host [B][iterations][2][K+3]. */
 int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le);

@@ -15,6 +15,7 @@ ARCH = "gfx950"
 
 LIB = os.path.join(PKG, "libturbo_mi355x.so")
 COMPAT = os.path.join(PKG, "libturbo_logmap_compat.so")
+DROPIN = os.path.join(PKG, "td_dropin_latency")   # examples/dropin_latency.cpp
 
 # -ffp-contract=off: the parity mode reproduces the reference's operation order exactly.
 # -fno-honor-nans: the decoder never produces a NaN from finite channel LLRs; without it hipcc
@@ -70,6 +71,11 @@ def build(force: bool = False, verbose: bool = False) -> None:
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,
               f"-L{PKG}", "-lturbo_mi355x", "-Wl,-rpath,$ORIGIN"])
+    # the unchanged caller's per-frame latency through the drop-in (bench.py `dropin`)
+    drv = os.path.join(REPO, "examples", "dropin_latency.cpp")
+    if os.path.exists(drv) and (force or _newer(DROPIN, [drv, COMPAT])):
+        _run(["g++", "-O2", "-std=c++17", "-o", DROPIN, drv, f"-L{PKG}", "-lturbo_logmap_compat", "-lturbo_mi355x",
+              "-Wl,-rpath,$ORIGIN"])
 
 
 if __name__ == "__main__":

@@ -60,6 +60,14 @@ struct td_handle {
     void* d_lut = nullptr;
     td::LaneTables* d_lane = nullptr;
     unsigned* d_slots = nullptr;   // per-CU occupancy bits of the turbo kernel (wg_pos)
+    unsigned long long* d_clk = nullptr;   // the last exact-schedule launch's clock samples (td_clock_read)
+    // td_decode_host's device staging (input stream, bits, optional Le), grown on demand and kept: the
+    // drop-in's TurboDecoding decodes one frame per call, so per-call allocations would be per frame
+    void* d_hin = nullptr;
+    uint8_t* d_hbits = nullptr;
+    void* d_hle = nullptr;
+    size_t hin_b = 0, hbits_b = 0, hle_b = 0;
+    std::vector<uint8_t> h_hbits;
     void* d_ws = nullptr;   // decode workspace
     std::vector<float> place_ms;   // td_reserve's placement trials (ms of one probe iteration each)
     int place_pick = -1;
@@ -526,6 +534,7 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.bits = d_bits;
     dp.le_dump = static_cast<T*>(d_le);
     dp.stamps = static_cast<unsigned long long*>(h->stamps);
+    dp.clk = h->d_clk;
     dp.K = h->p.K;
     dp.L = h->p.K + td::kMemory;
     dp.nT = (dp.L + td::window_steps() - 1) / td::window_steps();
@@ -799,7 +808,8 @@ int td_create(td_handle** out, const td_params* p)
         hipMalloc(&h->d_pinv, sizeof(int) * (p->K + td::kPermPad)) != hipSuccess ||
         hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess ||
         hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess ||
-        hipMalloc(&h->d_slots, sizeof(unsigned) * td::kCuSlotKeys) != hipSuccess) {
+        hipMalloc(&h->d_slots, sizeof(unsigned) * td::kCuSlotKeys) != hipSuccess ||
+        hipMalloc(&h->d_clk, 4 * sizeof(unsigned long long)) != hipSuccess) {
         td_destroy(h);
         return fail(TD_ENOMEM, "td_create: hipMalloc failed");
     }
@@ -807,6 +817,7 @@ int td_create(td_handle** out, const td_params* p)
     if (e == hipSuccess) e = hipMemset(h->d_pinv, 0, sizeof(int) * (p->K + td::kPermPad));
     if (e == hipSuccess) e = hipMemcpy(h->d_pi, h->pi.data(), sizeof(int) * p->K, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(h->d_slots, 0, sizeof(unsigned) * td::kCuSlotKeys);
+    if (e == hipSuccess) e = hipMemset(h->d_clk, 0, 4 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemcpy(h->d_lane, &h->lane, sizeof(td::LaneTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         std::vector<int> inv(p->K);
@@ -842,6 +853,10 @@ int td_destroy(td_handle* h)
     if (h->d_lut) (void)hipFree(h->d_lut);
     if (h->d_lane) (void)hipFree(h->d_lane);
     if (h->d_slots) (void)hipFree(h->d_slots);
+    if (h->d_clk) (void)hipFree(h->d_clk);
+    if (h->d_hin) (void)hipFree(h->d_hin);
+    if (h->d_hbits) (void)hipFree(h->d_hbits);
+    if (h->d_hle) (void)hipFree(h->d_hle);
     if (h->d_win) (void)hipFree(h->d_win);
     if (h->d_wws) (void)hipFree(h->d_wws);
     for (auto& tri : h->ev)
@@ -915,6 +930,20 @@ int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launch
     return TD_OK;
 }
 
+int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms)
+{
+    if (!h) return fail(TD_EINVAL, "td_clock_read: null handle");
+    TD_HIP(hipSetDevice(h->p.device));
+    TD_HIP(hipDeviceSynchronize());
+    unsigned long long v[4] = {};
+    TD_HIP(hipMemcpy(v, h->d_clk, sizeof v, hipMemcpyDeviceToHost));
+    const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);   // s_memrealtime: 100 MHz
+    if (v[3] <= v[1] || v[2] <= v[0]) return fail(TD_EINVAL, "td_clock_read: no exact-schedule decode recorded yet");
+    if (sclk_ghz) *sclk_ghz = cyc / ticks * 0.1;
+    if (span_ms) *span_ms = ticks * 1e-5;
+    return TD_OK;
+}
+
 int td_debug_set_stamps(td_handle* h, void* d_buf)
 {
     if (!h) return fail(TD_EINVAL, "td_debug_set_stamps: null handle");
@@ -981,6 +1010,8 @@ int td_debug_placement_rule(const float* ms, int n)
     return placement_fast_seen(std::vector<float>(ms, ms + n)) ? 1 : 0;
 }
 
+int td_window_steps(void) { return td::window_steps(); }
+
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
@@ -999,30 +1030,27 @@ int td_decode_host(td_handle* h, const void* llr, int B, int* out, void* le)
     const size_t in_b = (size_t)B * n * h->elem;
     const size_t bits_b = (size_t)B * it * K;
     const size_t le_b = le ? (size_t)B * it * 2 * L * h->elem : 0;
-    void *d_in = nullptr, *d_le = nullptr;
-    uint8_t* d_bits = nullptr;
-    int rc = TD_OK;
-    if (hipMalloc(&d_in, in_b) != hipSuccess || hipMalloc(&d_bits, bits_b) != hipSuccess ||
-        (le && hipMalloc(&d_le, le_b) != hipSuccess)) {
-        rc = fail(TD_ENOMEM, "td_decode_host: hipMalloc failed");
-    }
-    hipError_t e = hipSuccess;
-    if (!rc) e = hipMemcpy(d_in, llr, in_b, hipMemcpyHostToDevice);
-    if (!rc && e == hipSuccess) rc = td_decode_device(h, d_in, B, d_bits, 1, d_le, nullptr);
-    if (!rc && e == hipSuccess) e = hipDeviceSynchronize();
-    std::vector<uint8_t> hb;
-    if (!rc && e == hipSuccess) {
-        hb.resize(bits_b);
-        e = hipMemcpy(hb.data(), d_bits, bits_b, hipMemcpyDeviceToHost);
-    }
-    if (!rc && e == hipSuccess && le) e = hipMemcpy(le, d_le, le_b, hipMemcpyDeviceToHost);
-    if (!rc && e != hipSuccess) rc = hip_fail(e, "td_decode_host");
-    if (!rc)
-        for (size_t i = 0; i < bits_b; ++i) out[i] = hb[i];
-    if (d_in) (void)hipFree(d_in);
-    if (d_bits) (void)hipFree(d_bits);
-    if (d_le) (void)hipFree(d_le);
-    return rc;
+    // staging buffers kept by the handle (grown on demand), so a warm per-frame caller allocates nothing
+    auto grow = [](void** p, size_t& cap, size_t need) {
+        if (need <= cap) return hipSuccess;
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        cap = 0;
+        const hipError_t e = hipMalloc(p, need);
+        if (e == hipSuccess) cap = need;
+        return e;
+    };
+    if (grow(&h->d_hin, h->hin_b, in_b) != hipSuccess || grow(reinterpret_cast<void**>(&h->d_hbits), h->hbits_b, bits_b) != hipSuccess ||
+        (le && grow(&h->d_hle, h->hle_b, le_b) != hipSuccess))
+        return fail(TD_ENOMEM, "td_decode_host: hipMalloc failed");
+    TD_HIP(hipMemcpy(h->d_hin, llr, in_b, hipMemcpyHostToDevice));
+    const int rc = td_decode_device(h, h->d_hin, B, h->d_hbits, 1, le ? h->d_hle : nullptr, nullptr);
+    if (rc) return rc;
+    h->h_hbits.resize(bits_b);
+    TD_HIP(hipMemcpy(h->h_hbits.data(), h->d_hbits, bits_b, hipMemcpyDeviceToHost));   // waits for the decode (null stream)
+    if (le) TD_HIP(hipMemcpy(le, h->d_hle, le_b, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < bits_b; ++i) out[i] = h->h_hbits[i];
+    return TD_OK;
 }
 
 int td_siso_host(td_handle* h, const void* recs, const void* La, int terminated, void* LLR, int L, int B)

@@ -38,13 +38,14 @@ constexpr int kCuSlotKeys = 2048;    // (XCC, SE, SH, CU) keys of HW_ID
 // host sizes every buffer for the larger and reads the decode's own window count from
 // td::window_steps().
 constexpr int kWindowStepsMax = 15;
-// Alpha scratch (astore): group-major [G][L][64] (8 codewords x 8 states per step and group), plus
-// one window of the longest window length after the last group: the loader copies whole windows, so
-// the last group's last window reads past its L rows.  (Window-major and step-major layouts and pads
-// between the groups' streams were measured in round 3: none removed the placement modes of DESIGN.md
-// 3.2, and group-major had the fastest fast mode.)
-constexpr size_t astore_group_elems(int L) { return (size_t)L * 64; }
-constexpr size_t astore_elems(int G, int L) { return (size_t)G * astore_group_elems(L) + (size_t)kWindowStepsMax * 64; }
+// Alpha scratch (astore): group-major [G][L+1][64] (8 codewords x 8 states per step and group; row L
+// holds log-MAP's alpha_raw[.][L], whose max is beta's first tempmax), plus two windows of the longest
+// window length after the last group: the loader copies whole windows (and the first rows of the
+// window after the last), so the last group's copies read past its rows.  (Window-major and
+// step-major layouts and pads between the groups' streams were measured in round 3: none removed the
+// placement modes of DESIGN.md 3.2, and group-major had the fastest fast mode.)
+constexpr size_t astore_group_elems(int L) { return ((size_t)L + 1) * 64; }
+constexpr size_t astore_elems(int G, int L) { return (size_t)G * astore_group_elems(L) + (size_t)2 * kWindowStepsMax * 64; }
 
 template <typename T>
 struct DecodeParams {
@@ -63,6 +64,8 @@ struct DecodeParams {
     uint8_t* bits;              // decisions (see td_decode_device)
     T* le_dump;                 // nullable
     unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
+    unsigned long long* clk;    // nullable: workgroup 0's (shader clock, 100 MHz real time) at its start and
+                                // end, [4] (td_clock_read: the launch's sustained shader clock)
     int K, L, nT, G, B, iters, all_iters, algo;
     int role_cus;               // CU count for the second-round role rotation (wg_pos); 0 = off
     int occ3;                   // 1: large batches on three workgroups per CU where built (turbo_decode_kernel3)

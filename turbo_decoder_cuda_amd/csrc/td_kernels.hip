@@ -616,6 +616,34 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
 
+// Log-MAP B pass (kFoldConv): the two fold waves convert the staged window instead of the loader,
+// one tile item e per lane (wave A items 0 .. kTile/2-1, F1 the rest) -- tile_convert's arithmetic.
+#ifndef TD_FOLD_CONV
+#define TD_FOLD_CONV 0
+#endif
+template <int ALGO>
+constexpr bool kFoldConv = TD_FOLD_CONV != 0 && ALGO == 0;
+template <typename T>
+__device__ __forceinline__ void tile_convert_item(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int e)
+{
+    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
+    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);
+    T* g = &sm.G[t % 3][0][0][0];
+    const int k = e >> 3;
+    const T ys = sy[e], yp = sy[kTile + e];
+    const T la = la_at(src, t * kW + k, sy[2 * kTile + e]);
+    const T hla = la / (T)2;
+    g[4 * e] = (ys + yp) + hla;
+    g[4 * e + 1] = (ys - yp) + hla;
+    g[4 * e + 2] = ys;
+    g[4 * e + 3] = la;
+    if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
+        int* w = &sm.Wp[t % 3][0][0];
+        w[2 * k] = sw[k];
+        w[2 * k + 1] = sw[kWpInts + k];
+    }
+}
+
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
 
@@ -699,6 +727,72 @@ __device__ __forceinline__ void alpha_dma(Smem<T>& sm, const T* astore, const Ge
     }
 }
 
+// Log-MAP: the first DMA of alpha_dma for window t alone (its first kDmaBytes / (64 sizeof(T)) rows):
+// row 0 of the window after the last, i.e. alpha_raw[.][L] when the last window is full (L = 0 mod
+// kW), for tm_from_alpha of the last window.  One DMA instruction.
+template <typename T>
+__device__ __forceinline__ void alpha_dma_head(Smem<T>& sm, const T* astore, const Geom& gm, int t, int lane)
+{
+    const int slot = t % kAvSlots;
+    const char* src = reinterpret_cast<const char*>(astore + astore_window_off(gm.g, t, gm.L));
+    constexpr int row_bytes = kLanes * (int)sizeof(T);
+    const int b = lane * 16;
+    int off = b;
+    if constexpr (kFoldSwz<T>) {   // the same chunk placement as alpha_dma (the max reads a block in any order)
+        const int r = b / row_bytes, w = b % row_bytes;
+        constexpr int blk = 8 * (int)sizeof(T);
+        const int pc = ((w % blk) / 16 - av_rot<0>(r, w / blk)) & (kBlkChunks<T> - 1);
+        off = r * row_bytes + (w / blk) * blk + pc * 16;
+    }
+    dma16_stream(lds_addr(&sm.Av[slot][0][0]), src + off);
+}
+
+// max of the 8 states of one (row, codeword) block of the Av / Bv rings, read in any chunk order
+template <typename T>
+__device__ __forceinline__ T block_max(const T* blk)
+{
+    constexpr int E = 16 / (int)sizeof(T);
+    using V = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
+    T v[8];
+#pragma unroll
+    for (int p = 0; p < kBlkChunks<T>; ++p) {
+        const V x = *reinterpret_cast<const V*>(blk + p * E);
+        __builtin_memcpy(&v[p * E], &x, 16);
+    }
+    return vmax(vmax(vmax(v[0], v[1]), vmax(v[2], v[3])), vmax(vmax(v[4], v[5]), vmax(v[6], v[7])));
+}
+
+// Log-MAP, loader, B pass: beta's input tempmax[i+1] (:1019) of window t, for the window's steps
+// i = t kW + k: the reference's tempmax[i+1] = max_j alpha_raw[j][i+1] (:986-993, exact in any
+// order) over the alpha_raw rows the loader copied -- rows k+1 < kW from window t's Av slot, row kW
+// (= row 0 of window t+1) from the next window's slot (the last window: alpha_raw[.][L], row L of the
+// scratch, copied with window t or by alpha_dma_head).  Replaces the tempmax scratch stream.
+template <typename T>
+__device__ __forceinline__ void tm_from_alpha(Smem<T>& sm, int t, int lane)
+{
+    const T* a0 = &sm.Av[t % kAvSlots][0][0];
+    const T* a1 = &sm.Av[(t + 1) % kAvSlots][0][0];
+    T* d = &sm.tm[t & 1][0][0];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = lane + kLanes * q;
+        if (e < kTile) {
+            const int k = e >> 3, c = e & 7;
+            d[e] = block_max<T>((k + 1 < kW ? a0 + (k + 1) * kLanes : a1) + c * 8);
+        }
+    }
+}
+
+// Log-MAP folds: alpha[.][i] = alpha_raw[.][i] - tempmax[i] (:995-1000), the alpha wave's own
+// subtraction of the same exact max
+template <typename T>
+__device__ __forceinline__ void normalise8(T (&a)[8])
+{
+    const T m = vmax(vmax(vmax(a[0], a[1]), vmax(a[2], a[3])), vmax(vmax(a[4], a[5]), vmax(a[6], a[7])));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = a[j] - m;
+}
+
 // ---- recursion steps
 // Operands of one step are read from LDS ahead of the step group that uses them.
 template <typename T>
@@ -725,9 +819,13 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
 // alpha step i -> i+1 with i mod 3 = PH (log_map.cpp:975-1001).  `a` carries the UNnormalised
 // metric alpha_raw[.][i] of this lane's state; the step takes the reference's tempmax[i] =
 // max_j alpha_raw[j][i] (three DPP levels, the first one the partner exchange of this phase),
-// normalises (:986-1000), streams alpha[.][i] (by state, to `pa`) and tempmax[i] (to `ptm`) to
-// HBM scratch and returns alpha_raw[.][i+1].  fl(an - m) is exactly the partner's normalised
-// alpha, so the exchange is taken on the raw metric, ahead of the max.
+// normalises (:986-1000) and returns alpha_raw[.][i+1].  fl(an - m) is exactly the partner's
+// normalised alpha, so the exchange is taken on the raw metric, ahead of the max.
+// Scratch (round 4): log-MAP streams alpha_RAW[.][i] (by state, to `pa`) and nothing else -- the B
+// pass takes tempmax[i] = max_j alpha_raw[j][i] from the copied rows (beta: the loader's
+// tm_from_alpha; the folds: normalise8), the same exact max and the same subtraction, so the values
+// are bit-identical to streaming alpha[.][i] and tempmax; Max-Log-MAP, which keeps one row in three,
+// streams the normalised checkpoint rows and tempmax[i] (to `ptm`).
 // (A variant that read the max* row of the unnormalised difference ahead of the max, with an
 // exact redo of the window on a bucket mismatch, measured slower: 1098 vs 1203 Mbit/s.)
 template <typename T>
@@ -750,8 +848,12 @@ __device__ __forceinline__ StepHalf<T> alpha_issue(T a, const StepIn<T>& in, con
         const LutRow r = lut_row(h.d);
         lut_fields<T>(lut, r.o, h.thr, h.lo, h.hi);
     }
-    if ((kCkPh<ALGO> >> PH) & 1) gstore(pa, alpha);   // in the table read's shadow; only the kept phases (kCkPh)
-    gstore(ptm, m);
+    if constexpr (ALGO == 0) {
+        gstore(pa, a);   // in the table read's shadow
+    } else {
+        if ((kCkPh<ALGO> >> PH) & 1) gstore(pa, alpha);   // only the kept phases (kCkPh)
+        gstore(ptm, m);
+    }
     return h;
 }
 
@@ -845,10 +947,10 @@ __device__ __forceinline__ T sched_finish(T xs, T xp, T d, T thr, T lo, T hi)
 
 template <typename T, int K>
 struct AlphaSched {
-    // alpha step K (phase K mod 3) of a full window: a = alpha_raw[.][i] in, alpha_raw[.][i+1] out;
-    // op[K % 3] holds this step's operands, op[(K + 2) % 3] receives step K+2's
+    // alpha step K (phase K mod 3) of a full log-MAP window: a = alpha_raw[.][i] in, alpha_raw[.][i+1]
+    // out; op[K % 3] holds this step's operands, op[(K + 2) % 3] receives step K+2's
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
-                                               int c, const LaneConst<T>& lc, T* ga, T* gtm, T* ptm0)
+                                               int c, const LaneConst<T>& lc, T* ga)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
@@ -865,17 +967,16 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        gstore(ga + K * kLanes + lc.st_off[PH], alpha);   // log-MAP only
-        gstore(K == 0 ? ptm0 : gtm + c + (K - 1) * kCw, m);   // tempmax[i] at scratch index i - 1
+        gstore(ga + K * kLanes + lc.st_off[PH], a);   // alpha_raw[.][i]
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
-        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga, gtm, ptm0);
+        AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga);
     }
 };
 template <typename T>
 struct AlphaSched<T, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, T*)
+                                               const LaneConst<T>&, T*)
     {
     }
 };
@@ -941,8 +1042,7 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
             __builtin_amdgcn_sched_barrier(0);
-            astore_row<T, K>(sa, va[PH], alpha);
-            tm_keep<T, K>(tbh, m, stm);
+            astore_row<T, K>(sa, va[PH], a);   // alpha_raw[.][i]; no tempmax (alpha_issue)
             __builtin_amdgcn_sched_barrier(0);
             a = sched_finish(xs, xp, d, thr, lo, hi);
         } else {
@@ -1024,7 +1124,7 @@ __device__ __forceinline__ T alpha_window(T a, int t, int n, const Smem<T>& sm, 
             op[0] = alpha_in<T, 0>(sm, tb, 0, c, lc);
             op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
             TD_CHAIN_T0(c0);
-            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga, gtm, gtm + c - (t > 0 ? kCw : 0));
+            AlphaSched<T, 0>::run(a, op, sm, tb, lut, c, lc, ga);
             TD_CHAIN_ACC(c0);
             return a;
         }
@@ -1230,6 +1330,7 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
     } else {
         const T* av = &sm.Av[t % kAvSlots][k][c * 8];
         load_block<T>(av, k, a);
+        if constexpr (ALGO == 0) normalise8(a);   // the rows are alpha_raw (alpha_issue)
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1296,6 +1397,7 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     T a[8], b[8], t0[8], t1[8];
     load_block<T>(fl.Bv + s2 * (kW * kLanes), k, b);
     load_block<T>(fl.Av + s4 * (kW * kLanes), kFoldRows<ALGO> ? k : fl.arot, a);
+    if constexpr (ALGO == 0) normalise8(a);   // the rows are alpha_raw (alpha_issue)
     if constexpr (!kFoldRows<ALGO>) {   // alpha rows not kept: recomputed from the last kept one (fold_item)
         const T* gr = fl.Gr + s3 * (kW * kCw * 4);
         for (int q = 0; q < fl.rec; ++q) alpha_recompute<T, ALGO>(a, gr[q * kCw * 4], gr[q * kCw * 4 + 1], lut);
@@ -1427,7 +1529,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             a = alpha_window<T, ALGO>(a, t, window_len(gm, t), sm, lut_col(sm, lane), c, lc, ga0 + (size_t)t * aws,
                                       gtm0 + (size_t)t * kW * kCw, st ? st + 4 : nullptr);
             if (t == tl) {
-                gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
+                if constexpr (ALGO == 0) {   // alpha_raw[.][L] at row L (labels of phase L mod 3): its max is tempmax[L]
+                    const int ph = gm.L % 3;   // constant indices only: a runtime index into lc moves it to scratch
+                    ga0[(size_t)gm.L * kLanes + (ph == 0 ? lc.st_off[0] : ph == 1 ? lc.st_off[1] : lc.st_off[2])] = a;
+                } else {
+                    gtm0[(size_t)(gm.L - 1) * kCw + c] = group_max8(a);   // tempmax[L]
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // scratch visible to the loader
             }
             TD_STAMP(f1);
@@ -1478,6 +1585,58 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         constexpr int kB = kF + 1 + kAd;
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
+        if constexpr (ALGO == 0) {
+            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) converts the tiles of
+            // wa, copies alpha of wa-1 (folded at j+3) into LDS slot (wa-1) % 4 first and stages the
+            // tiles three windows lower, then waits until the previous iteration's alpha copy (window
+            // wa) has landed and forms beta's tempmax of wa from it (tm_from_alpha, beta next
+            // iteration): the copy has one iteration of latency instead of three, the tiles two.
+            auto bstep0 = [&](int j, int slot) {
+                TD_STAMP(b0);
+                const int wa = tl - j;
+                if constexpr (kFoldConv<ALGO>) {
+                    // the fold waves convert slot j % 3 this iteration (window wa, staged at j - 2); the
+                    // loader stages window wa - 2 into slot (j + 2) % 3, converted at j + 2
+                    if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+                    tile_dma(sm, slot == 0 ? 2 : slot - 1, src, dst, gm, max(min(wa - 2, tl - 3), 0), lane);
+                    TD_STAMP(bw);
+                    vm_wait<kAd + kF>();   // everything before this iteration has landed: the alpha copy of
+                                           // wa (tm_from_alpha) and the staging of wa - 1 (converted next)
+                } else {
+                if constexpr (!kDiag<kDiagNoBConvert>) {
+                    if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+                tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+                TD_STAMP(bw);
+                if (j == 0)
+                    vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
+                else
+                    vm_wait<kAd + 2 * kF>();   // the previous iteration's alpha copy (window wa) has landed
+                }
+                TD_STAMP(b1);
+                TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
+                if (wa >= 0) tm_from_alpha(sm, wa, lane);
+                wg_sync_lds();
+                TD_STAMP(b2);
+                TD_ACC(2, b0, b1);
+                TD_ACC(3, b1, b2);
+            };
+            if constexpr (kAd > 0) {
+                alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);      // folded at j = 2
+                alpha_dma_head<T>(sm, astore, gm, tl + 1, lane);   // alpha_raw[.][L] when the last window is full
+            }
+            TD_STAMP(p4);
+            TD_ACC(12, p3, p4);
+            for (int j = 0; j < nB; j += 3) {
+                bstep0(j, 0);
+                if (j + 1 < nB) bstep0(j + 1, 1);
+                if (j + 2 < nB) bstep0(j + 2, 2);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
+            return;
+        }
         auto bstep = [&](int j, int slot) {
             TD_STAMP(b0);
             const int wa = tl - j;
@@ -1616,6 +1775,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA) + lane;
         int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
+        const int ce = (wave == 0 ? 0 : kTile / 2) + lane;            // kFoldConv: this lane's tile item
+        const int cn = wave == 0 ? kTile / 2 : kTile - kTile / 2;     // ... and the wave's item count
         if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
@@ -1666,8 +1827,13 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
+            int cs = 0;   // staging slot of the window converted this iteration (kFoldConv): j % 3
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
+                if constexpr (kFoldConv<ALGO>) {
+                    if (lane < cn && wf >= 2) tile_convert_item(sm, cs, src, wf - 2, ce);
+                    cs = cs == 2 ? 0 : cs + 1;
+                }
                 if (!kDiag<kDiagNoFold> && lane < nfold)
                     fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
                 s3 = s3 == 0 ? 2 : s3 - 1;
@@ -1684,6 +1850,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
+            if constexpr (kFoldConv<ALGO>) {
+                if (lane < cn && wf >= 2 && wf - 2 <= tl - 3) tile_convert_item(sm, j % 3, src, wf - 2, ce);
+            }
             if (!kDiag<kDiagNoFold> && lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
@@ -1801,6 +1970,15 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
 #ifdef TD_STAMPS
     const unsigned long long k_cyc0 = __builtin_amdgcn_s_memtime(), k_rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    // launch clock: workgroup 0 reads the shader clock (s_memtime) and the 100 MHz real-time counter
+    // (s_memrealtime) at its start and end -- two scalar reads each, wave-uniform branch -- and its
+    // first lane writes them with one vector store (td_clock_read: the sustained clock of the launch)
+    const bool clk = p.clk && blockIdx.x == 0;
+    unsigned long long clk_c0 = 0, clk_r0 = 0;
+    if (clk) {
+        clk_c0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+    }
     // SISO pass s = 2*it + dec
     for (int s = 0; s < 2 * p.iters; ++s) {
         const int it = s >> 1, dec = s & 1;
@@ -1822,6 +2000,13 @@ __device__ __forceinline__ void turbo_decode_body(const DecodeParams<T>& p)
         TD_STAMP(s2);
         TD_ACC(9, s0, s1);
         TD_ACC(10, s1, s2);
+    }
+    if (clk) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            const ulonglong4 v = make_ulonglong4(clk_c0, clk_r0, c1, r1);
+            *reinterpret_cast<ulonglong4*>(p.clk) = v;
+        }
     }
 #ifdef TD_STAMPS
     st[6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
@@ -1875,7 +2060,8 @@ __global__ __launch_bounds__(kWaves * 64, 4) void turbo_decode_kernel4(DecodePar
 
 // td_reserve's workspace-placement probe (td_api.cpp place_ws): the same code as
 // turbo_decode_kernel under its own symbol, so that kernel traces and PMC passes of a decode list
-// the one-iteration probe launches apart from the decode's own launches.
+// the one-iteration probe launches apart from the decode's own launches.  (Decodes at three or four
+// workgroups per CU are probed with their own kernel, launch_turbo_algo.)
 template <typename T, int ALGO>
 __global__ __launch_bounds__(kWaves * 64, 2) void turbo_placement_probe_kernel(
     DecodeParams<T> p)
@@ -2398,7 +2584,10 @@ hipError_t launch_kernel4(const DecodeParams<T>& p, hipStream_t st)
 template <typename T, int ALGO>
 hipError_t launch_turbo_algo(const DecodeParams<T>& p, hipStream_t st, bool probe)
 {
-    const int occ = probe ? 2 : occupancy_pick<T, ALGO>(p);
+    // the placement probe times the kernel the decode will run: at two per CU under its own symbol (the
+    // traces list it apart); at three or four per CU (fp32 batches beyond one dispatch round) the
+    // decode's own kernel3 / kernel4
+    const int occ = occupancy_pick<T, ALGO>(p);
     if (occ == 4) {
         if constexpr (kOcc4<T, ALGO>) return launch_kernel4<T, ALGO>(p, st);
 #ifndef TD_W12_TU

@@ -162,6 +162,13 @@ class TurboCodec:
         N.check(N.lib().td_profile_read(self._h, C.byref(a), C.byref(b), C.byref(n)))
         return a.value, b.value, n.value
 
+    def clock(self):
+        """(sustained shader clock GHz, workgroup span ms) of the last exact-schedule turbo launch
+        (td_clock_read; synchronises the device)."""
+        g, s = C.c_double(), C.c_double()
+        N.check(N.lib().td_clock_read(self._h, C.byref(g), C.byref(s)))
+        return g.value, s.value
+
     # -- frame generator and error counts (main.cpp's channel, on the device) -------------
     def synth_seed(self, seed: int) -> None:
         """srand(seed) for the handle's frame stream (main.cpp:170)."""
