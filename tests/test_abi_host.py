@@ -123,6 +123,24 @@ def test_null_handle_calls_are_errors():
     assert L.td_reserve(None, 8) == N.TD_EINVAL
     assert L.td_decode_device(None, None, 1, None, 0, None, None) == N.TD_EINVAL
     assert L.td_destroy(None) == 0
+    assert L.td_clock_read(None, None, None) == N.TD_EINVAL
+
+
+def test_window_steps_is_the_kernel_window():
+    """td_window_steps: the exact kernel's window length (td_kernels.hip kW = 15), which
+    bench.traffic_model takes; a multiple of the rotating labels' period 3."""
+    W = N.lib().td_window_steps()
+    assert W == 15 and W % 3 == 0
+
+
+def test_dropin_latency_driver_built_and_linked():
+    """examples/dropin_latency.cpp (bench.py `dropin`) is built in-tree by build() against the compat
+    layer, i.e. it resolves the reference's C++ entry points from libturbo_logmap_compat.so."""
+    exe = os.path.join(PKG, "td_dropin_latency")
+    assert os.access(exe, os.X_OK), "run __graft_entry__.build()"
+    und = subprocess.run(["nm", "-D", "--undefined-only", exe], check=True, capture_output=True, text=True).stdout
+    for sym in ("_Z15TurboCodingInitv", "_Z13TurboDecodingPdPii", "_Z18TurboCodingReleasev"):
+        assert sym in und
 
 
 # ---------------------------------------------------------------- compat layer (C++ entry points)

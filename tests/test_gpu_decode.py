@@ -374,3 +374,24 @@ def test_tiny_K_vs_oracle(K, f1, f2, algo):
         ob, ol = O.turbo_decode(flow[b], K, f1, f2, iters, algo=oalgo)
         assert np.array_equal(bits[b], ob.astype(np.uint8)), f"codeword {b}"
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+
+
+@pytest.mark.parametrize("name", ["frames_K40_e0.0_s31.npz", "frames_K72_e0.5_s44.npz"])
+def test_dropin_latency_driver_matches_reference(tmp_path, name):
+    """examples/dropin_latency.cpp (bench.py's `dropin`): the unchanged caller's one-frame-per-call
+    TurboDecoding through libturbo_logmap_compat.so.  With TD_ITERATIONS = the golden frames' iteration
+    count, each frame's last-iteration row equals the compiled reference's (tests/golden), and the
+    driver reports a positive warm per-frame time."""
+    import json
+
+    d = np.load(os.path.join(GOLD, name))
+    K, nf, it = int(d["K"]), d["flow"].shape[0], int(d["iters"])
+    d["flow"].astype(np.float64).tofile(tmp_path / "flow.bin")
+    env = dict(os.environ, TD_ITERATIONS=str(it))
+    r = subprocess.run([os.path.join(PKG, "td_dropin_latency"), str(K), str(int(d["f1"])), str(int(d["f2"])), str(nf),
+                        str(tmp_path / "flow.bin"), str(tmp_path / "bits.bin")], capture_output=True, text=True,
+                       env=env, timeout=300, check=True)
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["frames"] == nf and rec["ms_per_frame"] > 0
+    bits = np.fromfile(tmp_path / "bits.bin", dtype=np.uint8).reshape(nf, K)
+    assert np.array_equal(bits, d["bits"][:, it - 1])

@@ -2,6 +2,8 @@
 captured into a hipGraph, both checked against the oracle."""
 import os
 
+import time
+
 import numpy as np
 import pytest
 
@@ -83,3 +85,30 @@ def test_graph_capture_between_eager_decodes():
             out_c = c.decode(xs[0], stream=sc)
         sc.synchronize()
         assert np.array_equal(out_c.cpu().numpy(), ref[0])
+
+
+def test_launch_clock_and_host_staging_reuse():
+    """td_clock_read after an exact-schedule decode: a sustained shader clock in the MI355X's range
+    (2.4 GHz peak) over a span no longer than the decode; td_decode_host keeps its device staging
+    across calls of different B (1, 5, 1) and every call decodes like the oracle."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2, iters = 1024, 31, 64, 3
+    _, flow = O.synth_batch(K, f1, f2, 0.4, 77, 5)
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        with pytest.raises(Exception):
+            c.clock()   # no exact-schedule launch yet
+        x = torch.from_numpy(flow).to(torch.device("cuda", 0))
+        t0 = time.perf_counter()
+        c.decode(x)
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        ghz, span = c.clock()
+        assert 0.5 < ghz < 3.0, ghz
+        assert 0 < span <= wall_ms + 1.0, (span, wall_ms)
+        for rows in (slice(0, 1), slice(0, 5), slice(3, 4)):
+            out = c.TurboDecoding(flow[rows])
+            for b, fr in enumerate(range(5)[rows]):
+                ob, _ = O.turbo_decode(flow[fr], K, f1, f2, iters)
+                assert np.array_equal(out[b].astype(np.uint8), ob.astype(np.uint8)), (rows, fr)
