@@ -107,7 +107,8 @@ def qpp_for(K):
 def window_steps() -> int:
     """Steps per window of the loaded library's exact-schedule kernel (td_window_steps)."""
     from turbo_decoder_cuda_amd import _native as N
-    return int(N.lib().td_window_steps())
+    L = N.lib()
+    return int(L.td_window_steps()) if hasattr(L, "td_window_steps") else 15   # older A/B builds: 15
 
 
 def load_traffic(cfg_key):

@@ -82,7 +82,8 @@ def lib() -> C.CDLL:
     L.td_debug_placement.argtypes = [P, C.POINTER(C.c_float), I, C.POINTER(C.c_int)]
     L.td_debug_placement_rule.argtypes = [C.POINTER(C.c_float), I]
     L.td_profile_read.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
-    L.td_clock_read.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    if hasattr(L, "td_clock_read"):   # measurement support (older A/B builds loaded by TD_LIB_PATH lack it)
+        L.td_clock_read.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.td_synth_seed.argtypes = [P, C.c_uint]
     L.td_rand_window.argtypes = [C.c_uint, C.c_ulonglong, P]
     L.td_synth_seek.argtypes = [P, C.c_ulonglong]

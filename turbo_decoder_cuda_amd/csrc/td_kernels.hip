@@ -616,34 +616,6 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
 
-// Log-MAP B pass (kFoldConv): the two fold waves convert the staged window instead of the loader,
-// one tile item e per lane (wave A items 0 .. kTile/2-1, F1 the rest) -- tile_convert's arithmetic.
-#ifndef TD_FOLD_CONV
-#define TD_FOLD_CONV 0
-#endif
-template <int ALGO>
-constexpr bool kFoldConv = TD_FOLD_CONV != 0 && ALGO == 0;
-template <typename T>
-__device__ __forceinline__ void tile_convert_item(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int e)
-{
-    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
-    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);
-    T* g = &sm.G[t % 3][0][0][0];
-    const int k = e >> 3;
-    const T ys = sy[e], yp = sy[kTile + e];
-    const T la = la_at(src, t * kW + k, sy[2 * kTile + e]);
-    const T hla = la / (T)2;
-    g[4 * e] = (ys + yp) + hla;
-    g[4 * e + 1] = (ys - yp) + hla;
-    g[4 * e + 2] = ys;
-    g[4 * e + 3] = la;
-    if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
-        int* w = &sm.Wp[t % 3][0][0];
-        w[2 * k] = sw[k];
-        w[2 * k + 1] = sw[kWpInts + k];
-    }
-}
-
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
 
@@ -1594,15 +1566,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             auto bstep0 = [&](int j, int slot) {
                 TD_STAMP(b0);
                 const int wa = tl - j;
-                if constexpr (kFoldConv<ALGO>) {
-                    // the fold waves convert slot j % 3 this iteration (window wa, staged at j - 2); the
-                    // loader stages window wa - 2 into slot (j + 2) % 3, converted at j + 2
-                    if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
-                    tile_dma(sm, slot == 0 ? 2 : slot - 1, src, dst, gm, max(min(wa - 2, tl - 3), 0), lane);
-                    TD_STAMP(bw);
-                    vm_wait<kAd + kF>();   // everything before this iteration has landed: the alpha copy of
-                                           // wa (tm_from_alpha) and the staging of wa - 1 (converted next)
-                } else {
                 if constexpr (!kDiag<kDiagNoBConvert>) {
                     if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 }
@@ -1614,7 +1577,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
                 else
                     vm_wait<kAd + 2 * kF>();   // the previous iteration's alpha copy (window wa) has landed
-                }
                 TD_STAMP(b1);
                 TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
                 if (wa >= 0) tm_from_alpha(sm, wa, lane);
@@ -1775,8 +1737,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA) + lane;
         int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
-        const int ce = (wave == 0 ? 0 : kTile / 2) + lane;            // kFoldConv: this lane's tile item
-        const int cn = wave == 0 ? kTile / 2 : kTile - kTile / 2;     // ... and the wave's item count
         if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
@@ -1827,13 +1787,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
-            int cs = 0;   // staging slot of the window converted this iteration (kFoldConv): j % 3
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
-                if constexpr (kFoldConv<ALGO>) {
-                    if (lane < cn && wf >= 2) tile_convert_item(sm, cs, src, wf - 2, ce);
-                    cs = cs == 2 ? 0 : cs + 1;
-                }
                 if (!kDiag<kDiagNoFold> && lane < nfold)
                     fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
                 s3 = s3 == 0 ? 2 : s3 - 1;
@@ -1850,9 +1805,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
-            if constexpr (kFoldConv<ALGO>) {
-                if (lane < cn && wf >= 2 && wf - 2 <= tl - 3) tile_convert_item(sm, j % 3, src, wf - 2, ce);
-            }
             if (!kDiag<kDiagNoFold> && lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
