@@ -31,8 +31,8 @@ torch.cuda.synchronize()
 c.profile(True)
 bits = c.decode(x)
 _, kms, _ = c.kernel_ms()
-NS = 14                 # td_kernels.hip kStampSlots
-NW = slots // NS        # waves per group: 4
+NW = 4                  # waves per group
+NS = slots // NW        # td_kernels.hip kStampSlots: 16 (14 before round 4)
 s = st.cpu().numpy().reshape(G, NW, NS).astype(np.float64)
 L = K + 3
 steps = 2 * iters * L
@@ -51,7 +51,9 @@ for w in range(NW):
     print(f"  {roles[w]:14s} per SISO-step: SISO calls {s[:, w, 9].mean() / steps:7.1f}  SISO-end barrier "
           f"{s[:, w, 10].mean() / steps:6.1f}  in-SISO unstamped {(s[:, w, 9] - s[:, w, 0:4].sum(axis=1)).mean() / steps:6.1f}"
           + (f"  F prologue {s[:, w, 11].mean() / steps:6.1f}" if NS > 11 else "")
-          + (f"  B prologue {s[:, w, 12].mean() / steps:6.1f}  first tile {s[:, w, 13].mean() / steps:6.1f}" if NS > 13 and w == 2 else ""))
+          + (f"  B prologue {s[:, w, 12].mean() / steps:6.1f}  first tile {s[:, w, 13].mean() / steps:6.1f}" if NS > 13 and w == 2 else "")
+          + (f"  B convert {s[:, w, 14].mean() / steps:6.1f}  DMA wait {s[:, w, 4].mean() / steps:6.1f}  tm_from_alpha "
+             f"{s[:, w, 15].mean() / steps:6.1f}" if NS > 15 and w == 2 else ""))
 hw = st.cpu().numpy().reshape(G, NW, NS)[:, :, 6].astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15

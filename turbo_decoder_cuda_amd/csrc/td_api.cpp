@@ -1015,7 +1015,7 @@ int td_window_steps(void) { return td::window_steps(); }
 int td_debug_stamp_slots(void)
 {
 #ifdef TD_STAMPS
-    return td::kGroupWaves * 14;   // [wave][slot] (td_kernels.hip kStampSlots)
+    return td::kGroupWaves * 16;   // [wave][slot] (td_kernels.hip kStampSlots)
 #else
     return 0;
 #endif

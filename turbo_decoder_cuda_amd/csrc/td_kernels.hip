@@ -325,6 +325,8 @@ template <typename T>
 constexpr int kStageBytes = kTileChunks<T> * 16;
 template <typename T>
 constexpr int kTmStageBytes = kStreamChunks<T> * 16;
+static_assert(3 * kTmStageBytes<double> <= kStageBytes<double> && 3 * kTmStageBytes<float> <= kStageBytes<float>,
+              "Max-Log-MAP's three tempmax stagings fit staging slot 3");
 
 template <typename T>
 struct Smem {
@@ -334,8 +336,10 @@ struct Smem {
     alignas(16) T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
-    alignas(16) unsigned char stage[3][kStageBytes<T>];     // loader: staged window inputs
-    alignas(16) unsigned char tmstage[3][kTmStageBytes<T>];  // loader: staged tempmax of a window
+    // loader: staged window inputs.  Slots 0-2 in the F pass; the log-MAP B pass rotates all four (its
+    // DMAs go out before the conversion of the slot they do not touch); Max-Log-MAP's B pass uses
+    // slots 0-2 and keeps its three staged tempmax windows in slot 3 (tm_stage)
+    alignas(16) unsigned char stage[4][kStageBytes<T>];
 };
 
 // Fold-input rows (Av, Bv): a (row, codeword) block holds the 8 states, 64 B in fp64 (4 chunks of
@@ -568,14 +572,14 @@ __device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, 
     const int e0 = min(lane, kStreamChunks<T> - 1) * E;
     const int i = min(max(t * kW + (e0 >> 3), 0), gm.L - 1);
     if (lane < kStreamChunks<T>)   // the lanes with a chunk only (kTmStageBytes)
-        dma16(lds_addr(&sm.tmstage[slot][0]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
+        dma16(lds_addr(&sm.stage[3][slot * kTmStageBytes<T>]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
 }
 
 // staged tempmax of window t -> its LDS slot (beta input)
 template <typename T>
 __device__ __forceinline__ void tm_convert(Smem<T>& sm, int slot, int t, int lane)
 {
-    const T* sv = reinterpret_cast<const T*>(&sm.tmstage[slot][0]);
+    const T* sv = reinterpret_cast<const T*>(&sm.stage[3][slot * kTmStageBytes<T>]);
     T* d = &sm.tm[t & 1][0][0];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1418,7 +1422,7 @@ constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
 // Max-Log-MAP.
 template <typename T>
 constexpr bool kRoleRemat = sizeof(T) == 4 || kW != 12;
-constexpr int kStampSlots = 14;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
+constexpr int kStampSlots = 16;  // per wave: F pass, F wait, B work, B wait, chain, XCC_ID, HW_ID, kernel
                                  // shader cycles, kernel realtime (100 MHz ticks), SISO calls, SISO-end
                                  // barriers, F prologue, loader B prologue, loader first tile (see diag)
 
@@ -1558,28 +1562,34 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
         if constexpr (ALGO == 0) {
-            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) converts the tiles of
-            // wa, copies alpha of wa-1 (folded at j+3) into LDS slot (wa-1) % 4 first and stages the
-            // tiles three windows lower, then waits until the previous iteration's alpha copy (window
-            // wa) has landed and forms beta's tempmax of wa from it (tm_from_alpha, beta next
-            // iteration): the copy has one iteration of latency instead of three, the tiles two.
+            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) first copies alpha of
+            // wa-1 (folded at j+3) into LDS slot (wa-1) % 4 and stages the tiles of wa-3 into staging
+            // slot (j+3) % 4 (converted at j+3), then converts the tiles of wa from slot j % 4 (staged
+            // at j-3), waits until the previous iteration's alpha copy (window wa) has landed and
+            // forms beta's tempmax of wa from it (tm_from_alpha, beta next iteration): the copy has
+            // one iteration of latency instead of three, the tiles two.  Four staging slots let the
+            // DMAs go out ahead of the conversion's LDS round trips.
             auto bstep0 = [&](int j, int slot) {
                 TD_STAMP(b0);
                 const int wa = tl - j;
+                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+                tile_dma(sm, slot == 0 ? 3 : slot - 1, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+                TD_STAMP(bc);
                 if constexpr (!kDiag<kDiagNoBConvert>) {
                     if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
-                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
-                tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
                 TD_STAMP(bw);
+                TD_ACC(14, bc, bw);   // stamps build: the loader's slot 14 is its B-pass tile conversion
                 if (j == 0)
                     vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
                 else
                     vm_wait<kAd + 2 * kF>();   // the previous iteration's alpha copy (window wa) has landed
-                TD_STAMP(b1);
-                TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
+                TD_STAMP(bt);
+                TD_ACC(4, bw, bt);   // stamps build: the loader's slot 4 is its B-pass DMA wait
                 if (wa >= 0) tm_from_alpha(sm, wa, lane);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                TD_STAMP(b1);
+                TD_ACC(15, bt, b1);   // ... slot 15 its tempmax formation (tm_from_alpha, to its writes' completion)
                 wg_sync_lds();
                 TD_STAMP(b2);
                 TD_ACC(2, b0, b1);
@@ -1591,10 +1601,11 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             }
             TD_STAMP(p4);
             TD_ACC(12, p3, p4);
-            for (int j = 0; j < nB; j += 3) {
+            for (int j = 0; j < nB; j += 4) {
                 bstep0(j, 0);
                 if (j + 1 < nB) bstep0(j + 1, 1);
                 if (j + 2 < nB) bstep0(j + 2, 2);
+                if (j + 3 < nB) bstep0(j + 3, 3);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
             return;
