@@ -315,18 +315,51 @@ constexpr int kStreamChunks = kTile * (int)sizeof(T) / 16;   // chunks of one [k
 constexpr int kWpChunks = kW % 4 == 0 ? kW / 4 : (kW + 3 + 3) / 4;
 constexpr int kWpInts = 4 * kWpChunks;   // staged ints per table
 static_assert(kW % 4 == 0 || kWpInts >= kW + 3, "a window's write positions lie within its staged chunks");
+// Lane-aligned staging (round 4): each stream occupies a power-of-two run of P lanes of a DMA (fp64:
+// 64, one stream per DMA; fp32: 32, two per DMA), so a lane's stream and chunk are a shift and a
+// mask of its lane index -- no per-lane division by the chunk count in the loader's address math
+// (it had been recomputed in every B-pass iteration).  The write-position chunks take the spare
+// lanes: fp64 the P - nc lanes at the end of each stream run, fp32 the fourth run of 32.
 template <typename T>
-constexpr int kTileChunks = 3 * kStreamChunks<T> + 2 * kWpChunks;
+constexpr int kStreamLanes = kStreamChunks<T> > 32 ? 64 : 32;                // P
 template <typename T>
-constexpr int kTileDma = (kTileChunks<T> + kLanes - 1) / kLanes;   // DMA instructions per staged window
-// Staging slots hold exactly a window's chunks: the last DMA of a window (and the tempmax DMA) run on
-// the lanes that have a chunk only, so the slots carry no spare lanes' landing space.
+constexpr int kStreamsPerDma = kLanes / kStreamLanes<T>;
+static_assert(kStreamChunks<double> <= 64 && kStreamChunks<float> <= 32, "a stream fits its lane run");
 template <typename T>
-constexpr int kStageBytes = kTileChunks<T> * 16;
+constexpr bool kWpInSpare = kStreamsPerDma<T> == 1;   // fp64: write positions in the stream runs' spare lanes
+template <typename T>
+constexpr int kWpPerRun = kStreamLanes<T> - kStreamChunks<T>;   // fp64: spare lanes per stream run
+static_assert(!kWpInSpare<double> || 3 * kWpPerRun<double> >= 2 * kWpChunks, "the write positions fit the spare lanes");
+static_assert(kStreamsPerDma<float> != 2 || 2 * kWpChunks <= 32, "the write positions fit the fourth lane run");
+template <typename T>
+constexpr int kTileDma = kWpInSpare<T> ? 3 : 2;   // DMA instructions per staged window
+// lanes of the last DMA that carry a chunk (the slot ends there)
+template <typename T>
+constexpr int kLastDmaLanes = kWpInSpare<T> ? kLanes : 32 + 2 * kWpChunks;
+template <typename T>
+constexpr int kStageBytes = (kTileDma<T> - 1) * kDmaBytes + kLastDmaLanes<T> * 16;
+// byte offset in a staging slot of stream s (0 ys, 1 yp, 2 La; element e at + e * sizeof(T)) ...
+template <typename T>
+constexpr int stage_stream_off(int s)
+{
+    return ((s / kStreamsPerDma<T>) * kLanes + (s % kStreamsPerDma<T>) * kStreamLanes<T>) * 16;
+}
+// ... and of write-position int n (n < kWpInts: pi-or-pinv from the window's aligned chunk, then pi)
+template <typename T>
+__device__ __forceinline__ int stage_wp_off(int n)
+{
+    if constexpr (kWpInSpare<T>) {
+        constexpr int per = 4 * kWpPerRun<T>;   // ints per stream run's spare lanes
+        return (n / per) * kDmaBytes + kStreamChunks<T> * 16 + (n % per) * 4;
+    } else {
+        return kDmaBytes + 32 * 16 + n * 4;
+    }
+}
 template <typename T>
 constexpr int kTmStageBytes = kStreamChunks<T> * 16;
 static_assert(3 * kTmStageBytes<double> <= kStageBytes<double> && 3 * kTmStageBytes<float> <= kStageBytes<float>,
               "Max-Log-MAP's three tempmax stagings fit staging slot 3");
+static_assert(kStageBytes<double> % 16 == 0 && kStageBytes<float> % 16 == 0, "16-byte staging slots");
 
 template <typename T>
 struct Smem {
@@ -537,16 +570,16 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
                                          const Geom& gm, int t, int lane)
 {
     constexpr int E = 16 / (int)sizeof(T);   // elements per chunk (a chunk never crosses a step row)
-    constexpr int nc = kStreamChunks<T>;
+    constexpr int nc = kStreamChunks<T>, P = kStreamLanes<T>;
     const int* pperm = dst.ext_mode == 3 ? gm.pinv : gm.pi;
     const unsigned base = lds_addr(&sm.stage[slot][0]);
     const int tc = max(t, 0);
+    const int u = lane & (P - 1);            // chunk within the lane's stream run
 #pragma unroll
     for (int q = 0; q < kTileDma<T>; ++q) {
-        const int ch = q * kLanes + lane;
-        // stream chunks: s = 0 ys, 1 yp, 2 La
-        const int cs = min(ch, 3 * nc - 1);
-        const int s = cs / nc, e0 = (cs - s * nc) * E;
+        const int sg = q * kStreamsPerDma<T> + lane / P;   // the lane's run: 0 ys, 1 yp, 2 La, 3 (fp32) positions
+        const int s = min(sg, 2);
+        const int e0 = min(u, nc - 1) * E;
         const int i = min(tc * kW + (e0 >> 3), gm.L - 1);
         // base of stream s by arithmetic (a select chain over the three pointers becomes a
         // runtime-indexed private array, i.e. scratch)
@@ -554,13 +587,16 @@ __device__ __forceinline__ void tile_dma(Smem<T>& sm, int slot, const SisoSrc<T>
         const size_t sb = a0 + (size_t)(s == 1) * (a1 - a0) + (size_t)(s == 2) * (a2 - a0);
         const size_t row = s == 2 ? (size_t)gm.g * src.la_cap + min(i, src.la_cap - 1) : (size_t)gm.g * gm.L + i;
         const char* ps = reinterpret_cast<const char*>(sb + (row * kCw + (e0 & 7)) * sizeof(T));
-        // write-position chunks: r < kWpChunks pi-or-pinv, else pi; from the aligned chunk at or
-        // below the window's first step
-        const int r = min(max(ch - 3 * nc, 0), 2 * kWpChunks - 1);
+        // write-position chunk r (r < kWpChunks pi-or-pinv, else pi) from the aligned chunk at or below
+        // the window's first step: fp64 in the spare lanes u >= nc of each run, fp32 in run 3
+        const int rr = kWpInSpare<T> ? sg * kWpPerRun<T> + (u - nc) : u;
+        const int r = min(max(rr, 0), 2 * kWpChunks - 1);
         const int* pb = r < kWpChunks ? pperm : gm.pi;
         const char* pw = reinterpret_cast<const char*>(pb + ((tc * kW) & ~3) + (r % kWpChunks) * 4);
-        if (q + 1 < kTileDma<T> || ch < kTileChunks<T>)   // the last DMA: the lanes with a chunk only
-            dma16(base + q * kDmaBytes, ch < 3 * nc ? ps : pw);
+        const bool stream = sg < 3 && u < nc;
+        const bool wp = kWpInSpare<T> ? (u >= nc && rr < 2 * kWpChunks) : (sg == 3 && u < 2 * kWpChunks);
+        if ((q + 1 < kTileDma<T> && kWpInSpare<T>) || stream || wp)   // the lanes with a chunk only
+            dma16(base + q * kDmaBytes, stream ? ps : pw);
     }
 }
 
@@ -593,10 +629,11 @@ __device__ __forceinline__ void tm_convert(Smem<T>& sm, int slot, int t, int lan
 template <typename T>
 __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int lane)
 {
-    const T* sy = reinterpret_cast<const T*>(&sm.stage[slot][0]);
-    const T* sp = sy + kTile;
-    const T* sl = sy + 2 * kTile;
-    const int* sw = reinterpret_cast<const int*>(sy + 3 * kTile) + ((t * kW) & 3);   // [kWpInts] pi-or-pinv, then [kWpInts] pi
+    const unsigned char* sb = &sm.stage[slot][0];
+    const T* sy = reinterpret_cast<const T*>(sb + stage_stream_off<T>(0));
+    const T* sp = reinterpret_cast<const T*>(sb + stage_stream_off<T>(1));
+    const T* sl = reinterpret_cast<const T*>(sb + stage_stream_off<T>(2));
+    const int wo = (t * kW) & 3;   // the window's first position within its aligned chunk
     T* g = &sm.G[t % 3][0][0][0];
     int* w = &sm.Wp[t % 3][0][0];
 #pragma unroll
@@ -612,13 +649,43 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
             g[4 * e + 2] = ys;
             g[4 * e + 3] = la;
             if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
-                w[2 * k] = sw[k];
-                w[2 * k + 1] = sw[kWpInts + k];
+                w[2 * k] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(wo + k));
+                w[2 * k + 1] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(kWpInts + wo + k));
             }
         }
     }
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
+
+// Log-MAP B pass, TD_FOLD_CONV (A/B): the two fold waves convert the staged window instead of the
+// loader, one tile item e per lane (wave A items 0 .. kTile/2-1, F1 the rest) -- tile_convert's
+// arithmetic; the staging keeps its three iterations of latency (four slots).
+#ifndef TD_FOLD_CONV
+#define TD_FOLD_CONV 0
+#endif
+template <int ALGO>
+constexpr bool kFoldConv = TD_FOLD_CONV != 0 && ALGO == 0;
+template <typename T>
+__device__ __forceinline__ void tile_convert_item(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int e)
+{
+    const unsigned char* sb = &sm.stage[slot][0];
+    const int wo = (t * kW) & 3;
+    T* g = &sm.G[t % 3][0][0][0];
+    const int k = e >> 3;
+    const T ys = reinterpret_cast<const T*>(sb + stage_stream_off<T>(0))[e];
+    const T yp = reinterpret_cast<const T*>(sb + stage_stream_off<T>(1))[e];
+    const T la = la_at(src, t * kW + k, reinterpret_cast<const T*>(sb + stage_stream_off<T>(2))[e]);
+    const T hla = la / (T)2;
+    g[4 * e] = (ys + yp) + hla;
+    g[4 * e + 1] = (ys - yp) + hla;
+    g[4 * e + 2] = ys;
+    g[4 * e + 3] = la;
+    if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
+        int* w = &sm.Wp[t % 3][0][0];
+        w[2 * k] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(wo + k));
+        w[2 * k + 1] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(kWpInts + wo + k));
+    }
+}
 
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
@@ -1575,7 +1642,7 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                 if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
                 tile_dma(sm, slot == 0 ? 3 : slot - 1, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
                 TD_STAMP(bc);
-                if constexpr (!kDiag<kDiagNoBConvert>) {
+                if constexpr (!kDiag<kDiagNoBConvert> && !kFoldConv<ALGO>) {
                     if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 }
                 TD_STAMP(bw);
@@ -1748,6 +1815,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA) + lane;
         int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
+        const int ce = (wave == 0 ? 0 : kTile / 2) + lane;            // kFoldConv: this lane's tile item
+        const int cn = wave == 0 ? kTile / 2 : kTile - kTile / 2;     // ... and the wave's item count
         if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
@@ -1798,8 +1867,13 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
+            int cs = 3;   // kFoldConv: staging slot of the window converted this iteration, j % 4
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
+                if constexpr (kFoldConv<ALGO>) {
+                    if (lane < cn && wf >= 2) tile_convert_item(sm, cs, src, wf - 2, ce);
+                    cs = (cs + 1) & 3;
+                }
                 if (!kDiag<kDiagNoFold> && lane < nfold)
                     fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
                 s3 = s3 == 0 ? 2 : s3 - 1;
@@ -1816,6 +1890,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
+            if constexpr (kFoldConv<ALGO>) {
+                if (lane < cn && j >= 3 && wf >= 2) tile_convert_item(sm, j & 3, src, wf - 2, ce);
+            }
             if (!kDiag<kDiagNoFold> && lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
