@@ -295,8 +295,11 @@ __device__ __forceinline__ void lane_setup(const LaneTables* lt, int lane, LaneC
 // the B pass from one checkpoint per window, -10 % at B = 4096; the fold lanes loading their alpha
 // blocks from HBM instead of the Av ring, -9 %; F1 folding with one E_seq chain per lane, level.)
 constexpr int kWaves = kGroupWaves;                  // waves per codeword group
-constexpr int kFoldA = kTile / 2;                    // items per folding wave (A and F1) per window
-static_assert(kFoldA <= kLanes, "one fold item per lane");
+// items of fold wave A (beside the other workgroup's loader) per window; F1 (beside its beta) the
+// rest.  64 / 56 measured level with 60 / 60 (round 4), as 40/56 .. 56/40 against 48/48 did with
+// 12-step windows (round 3).
+constexpr int kFoldA = kTile / 2;
+static_assert(kFoldA <= kLanes && kTile - kFoldA <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 // every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
 template <int ALGO>
@@ -369,9 +372,8 @@ struct Smem {
     alignas(16) T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
-    // loader: staged window inputs.  Slots 0-2 in the F pass; the log-MAP B pass rotates all four (its
-    // DMAs go out before the conversion of the slot they do not touch); Max-Log-MAP's B pass uses
-    // slots 0-2 and keeps its three staged tempmax windows in slot 3 (tm_stage)
+    // loader: staged window inputs, slots 0-2 (window t in slot t % 3); Max-Log-MAP keeps its three
+    // staged tempmax windows in slot 3
     alignas(16) unsigned char stage[4][kStageBytes<T>];
 };
 
@@ -656,36 +658,6 @@ __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSr
     }
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
-
-// Log-MAP B pass, TD_FOLD_CONV (A/B): the two fold waves convert the staged window instead of the
-// loader, one tile item e per lane (wave A items 0 .. kTile/2-1, F1 the rest) -- tile_convert's
-// arithmetic; the staging keeps its three iterations of latency (four slots).
-#ifndef TD_FOLD_CONV
-#define TD_FOLD_CONV 0
-#endif
-template <int ALGO>
-constexpr bool kFoldConv = TD_FOLD_CONV != 0 && ALGO == 0;
-template <typename T>
-__device__ __forceinline__ void tile_convert_item(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int e)
-{
-    const unsigned char* sb = &sm.stage[slot][0];
-    const int wo = (t * kW) & 3;
-    T* g = &sm.G[t % 3][0][0][0];
-    const int k = e >> 3;
-    const T ys = reinterpret_cast<const T*>(sb + stage_stream_off<T>(0))[e];
-    const T yp = reinterpret_cast<const T*>(sb + stage_stream_off<T>(1))[e];
-    const T la = la_at(src, t * kW + k, reinterpret_cast<const T*>(sb + stage_stream_off<T>(2))[e]);
-    const T hla = la / (T)2;
-    g[4 * e] = (ys + yp) + hla;
-    g[4 * e + 1] = (ys - yp) + hla;
-    g[4 * e + 2] = ys;
-    g[4 * e + 3] = la;
-    if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
-        int* w = &sm.Wp[t % 3][0][0];
-        w[2 * k] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(wo + k));
-        w[2 * k + 1] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(kWpInts + wo + k));
-    }
-}
 
 // the last window starts at most at step L-1 = K+kMemory-1 and stages kW write positions from there
 static_assert(kMemory + kWpInts - 1 <= kPermPad, "write-position chunks stay within the padded tables");
@@ -1629,24 +1601,25 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         TD_STAMP(p3);
         vm_wait<0>();   // the F pass's last (unused) staging
         if constexpr (ALGO == 0) {
-            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) first copies alpha of
-            // wa-1 (folded at j+3) into LDS slot (wa-1) % 4 and stages the tiles of wa-3 into staging
-            // slot (j+3) % 4 (converted at j+3), then converts the tiles of wa from slot j % 4 (staged
-            // at j-3), waits until the previous iteration's alpha copy (window wa) has landed and
-            // forms beta's tempmax of wa from it (tm_from_alpha, beta next iteration): the copy has
-            // one iteration of latency instead of three, the tiles two.  Four staging slots let the
-            // DMAs go out ahead of the conversion's LDS round trips.
+            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) converts the tiles of
+            // wa, copies alpha of wa-1 (folded at j+3) into LDS slot (wa-1) % 4 first and stages the
+            // tiles three windows lower, then waits until the previous iteration's alpha copy (window
+            // wa) has landed and forms beta's tempmax of wa from it (tm_from_alpha, beta next
+            // iteration): the copy has one iteration of latency instead of three, the tiles two.
+            // (Issuing the DMAs ahead of the conversion, with a fourth staging slot, measured 0.8 %
+            // slower: the conversion's LDS reads then meet the DMAs' LDS writes.)
             auto bstep0 = [&](int j, int slot) {
                 TD_STAMP(b0);
                 const int wa = tl - j;
-                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
-                tile_dma(sm, slot == 0 ? 3 : slot - 1, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
-                TD_STAMP(bc);
-                if constexpr (!kDiag<kDiagNoBConvert> && !kFoldConv<ALGO>) {
+                if constexpr (!kDiag<kDiagNoBConvert>) {
                     if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
                 }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+                TD_STAMP(bc);
+                TD_ACC(14, b0, bc);   // stamps build: the loader's slot 14 is its B-pass tile conversion
+                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+                tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
                 TD_STAMP(bw);
-                TD_ACC(14, bc, bw);   // stamps build: the loader's slot 14 is its B-pass tile conversion
                 if (j == 0)
                     vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
                 else
@@ -1668,11 +1641,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             }
             TD_STAMP(p4);
             TD_ACC(12, p3, p4);
-            for (int j = 0; j < nB; j += 4) {
+            for (int j = 0; j < nB; j += 3) {
                 bstep0(j, 0);
                 if (j + 1 < nB) bstep0(j + 1, 1);
                 if (j + 2 < nB) bstep0(j + 2, 2);
-                if (j + 3 < nB) bstep0(j + 3, 3);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
             return;
@@ -1815,8 +1787,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
         int fe = (wave == 0 ? 0 : kFoldA) + lane;
         int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
-        const int ce = (wave == 0 ? 0 : kTile / 2) + lane;            // kFoldConv: this lane's tile item
-        const int cn = wave == 0 ? kTile / 2 : kTile - kTile / 2;     // ... and the wave's item count
         if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
@@ -1867,13 +1837,8 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                                               : nullptr;
             const T* lut = lut_col(sm, lane);
             int wf = tl - 1, s3 = wf % 3, s4 = wf % kAvSlots, s2 = wf & 1;
-            int cs = 3;   // kFoldConv: staging slot of the window converted this iteration, j % 4
             for (int j = 3; j < nB; ++j, --wf) {
                 TD_STAMP(b0);
-                if constexpr (kFoldConv<ALGO>) {
-                    if (lane < cn && wf >= 2) tile_convert_item(sm, cs, src, wf - 2, ce);
-                    cs = (cs + 1) & 3;
-                }
                 if (!kDiag<kDiagNoFold> && lane < nfold)
                     fold_item_fast<T, ALGO>(fl, lut, s3, s4, s2, wf * kW, dst.ext_len, gm.K);
                 s3 = s3 == 0 ? 2 : s3 - 1;
@@ -1890,9 +1855,6 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         for (int j = j0; j < nB; ++j) {
             TD_STAMP(b0);
             const int wf = tl - j + 2;
-            if constexpr (kFoldConv<ALGO>) {
-                if (lane < cn && j >= 3 && wf >= 2) tile_convert_item(sm, j & 3, src, wf - 2, ce);
-            }
             if (!kDiag<kDiagNoFold> && lane < nfold && wf >= 0 && wf <= tl && (fe >> 3) < window_len(gm, wf))
                 fold_item<T, ALGO>(sm, lut_col(sm, lane), wf, fe, dst, gm);
             TD_STAMP(b1);
