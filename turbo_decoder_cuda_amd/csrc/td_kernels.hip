@@ -352,8 +352,8 @@ template <typename T>
 __device__ __forceinline__ int stage_wp_off(int n)
 {
     if constexpr (kWpInSpare<T>) {
-        constexpr int per = 4 * kWpPerRun<T>;   // ints per stream run's spare lanes
-        return (n / per) * kDmaBytes + kStreamChunks<T> * 16 + (n % per) * 4;
+        constexpr unsigned per = 4 * kWpPerRun<T>;   // ints per stream run's spare lanes
+        return (int)(((unsigned)n / per) * kDmaBytes + kStreamChunks<T> * 16 + ((unsigned)n % per) * 4);
     } else {
         return kDmaBytes + 32 * 16 + n * 4;
     }
@@ -368,7 +368,7 @@ template <typename T>
 struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
-    int Wp[3][kW][2];          // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
+    alignas(8) int Wp[3][kW][2];   // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
     alignas(16) T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
     alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
@@ -631,31 +631,40 @@ __device__ __forceinline__ void tm_convert(Smem<T>& sm, int slot, int t, int lan
 template <typename T>
 __device__ __forceinline__ void tile_convert(Smem<T>& sm, int slot, const SisoSrc<T>& src, int t, int lane)
 {
+    // Every LDS read is issued before the first write, and no lane is masked: the compiler cannot tell
+    // the staging slot from the rings, so a write between two reads made it wait for the write, and a
+    // lane-masked write put a branch around it -- written per pass and per write position, the
+    // conversion was six serial LDS round trips a window (87 cycles a step of the loader's 182 at
+    // B = 8, round 4 stamps).  Lanes past the window (second pass) and past its steps (positions)
+    // repeat the last item: the same values to the same address.
     const unsigned char* sb = &sm.stage[slot][0];
     const T* sy = reinterpret_cast<const T*>(sb + stage_stream_off<T>(0));
     const T* sp = reinterpret_cast<const T*>(sb + stage_stream_off<T>(1));
     const T* sl = reinterpret_cast<const T*>(sb + stage_stream_off<T>(2));
     const int wo = (t * kW) & 3;   // the window's first position within its aligned chunk
-    T* g = &sm.G[t % 3][0][0][0];
-    int* w = &sm.Wp[t % 3][0][0];
+    const int e[2] = {lane, min(lane + kLanes, kTile - 1)};
+    const int kp = min(lane, kW - 1);   // this lane's step for the write positions
+    T ys[2], yp[2], lr[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-        const int e = lane + kLanes * q;
-        if (e < kTile) {
-            const int k = e >> 3;
-            const T ys = sy[e], yp = sp[e];
-            const T la = la_at(src, t * kW + k, sl[e]);
-            const T hla = la / (T)2;
-            g[4 * e] = (ys + yp) + hla;
-            g[4 * e + 1] = (ys - yp) + hla;
-            g[4 * e + 2] = ys;
-            g[4 * e + 3] = la;
-            if ((e & 7) == 0) {   // one entry per step: every codeword has the same positions
-                w[2 * k] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(wo + k));
-                w[2 * k + 1] = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(kWpInts + wo + k));
-            }
-        }
+        ys[q] = sy[e[q]];
+        yp[q] = sp[e[q]];
+        lr[q] = sl[e[q]];
     }
+    const int w0 = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(wo + kp));
+    const int w1 = *reinterpret_cast<const int*>(sb + stage_wp_off<T>(kWpInts + wo + kp));
+    T* g = &sm.G[t % 3][0][0][0];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const T la = la_at(src, t * kW + (e[q] >> 3), lr[q]);
+        const T hla = la / (T)2;
+        g[4 * e[q]] = (ys[q] + yp[q]) + hla;
+        g[4 * e[q] + 1] = (ys[q] - yp[q]) + hla;
+        g[4 * e[q] + 2] = ys[q];
+        g[4 * e[q] + 3] = la;
+    }
+    // one entry per step (every codeword has the same positions), both tables as one 8-byte write
+    *reinterpret_cast<int2*>(&sm.Wp[t % 3][kp][0]) = make_int2(w0, w1);
 }
 static_assert(kTile <= 2 * kLanes, "tile_convert covers a window in two passes");
 
@@ -788,14 +797,15 @@ __device__ __forceinline__ void tm_from_alpha(Smem<T>& sm, int t, int lane)
     const T* a0 = &sm.Av[t % kAvSlots][0][0];
     const T* a1 = &sm.Av[(t + 1) % kAvSlots][0][0];
     T* d = &sm.tm[t & 1][0][0];
+    T m[2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = lane + kLanes * q;
-        if (e < kTile) {
-            const int k = e >> 3, c = e & 7;
-            d[e] = block_max<T>((k + 1 < kW ? a0 + (k + 1) * kLanes : a1) + c * 8);
-        }
+    for (int q = 0; q < 2; ++q) {   // lanes past the window (second pass) repeat the last item
+        const int e = min(lane + kLanes * q, kTile - 1);
+        const int k = e >> 3, c = e & 7;
+        m[q] = block_max<T>((k + 1 < kW ? a0 + (k + 1) * kLanes : a1) + c * 8);
     }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) d[min(lane + kLanes * q, kTile - 1)] = m[q];
 }
 
 // Log-MAP folds: alpha[.][i] = alpha_raw[.][i] - tempmax[i] (:995-1000), the alpha wave's own
