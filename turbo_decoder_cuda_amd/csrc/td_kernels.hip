@@ -1461,6 +1461,26 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #define TD_STAMP(v)
 #define TD_ACC(slot, a, b)
 #endif
+// Which wave loads in the B pass: 2 (F0, the F pass's loader) or 3 (F1, beside the other
+// workgroup's beta; F0 then folds beside the other workgroup's fold wave A).  Log-MAP keeps F0
+// (beta bounds its B pass; F1 measured 0.5 % slower, fp32 0.8 %); Max-Log-MAP, whose B pass the
+// folds and the loader bound, moves it to F1 (+3.0 %, config 3).  The F pass then stages nothing
+// past the last window (kFSkip), so no F-pass DMA is in flight when F1 starts staging.
+#ifndef TD_BLOADER_LOG
+#define TD_BLOADER_LOG 2
+#endif
+#ifndef TD_BLOADER_MAX
+#define TD_BLOADER_MAX 3
+#endif
+#ifndef TD_FSKIP
+#define TD_FSKIP 0
+#endif
+template <int ALGO>
+constexpr int kBLoaderWave = ALGO == 1 ? TD_BLOADER_MAX : TD_BLOADER_LOG;
+template <int ALGO>
+constexpr bool kFSkip = TD_FSKIP != 0 || kBLoaderWave<ALGO> == 3;
+static_assert(TD_BLOADER_LOG == 2 || TD_BLOADER_LOG == 3, "B-pass loader: wave 2 or 3");
+static_assert(TD_BLOADER_MAX == 2 || TD_BLOADER_MAX == 3, "B-pass loader: wave 2 or 3");
 constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
 // The lane index made opaque at the start of every SISO (role remat), so that the compiler cannot
 // hoist the roles' lane-derived addresses (fold lanes, alpha store offsets, ...) out of the SISO loop,
@@ -1479,6 +1499,112 @@ constexpr int kStampSlots = 16;  // per wave: F pass, F wait, B work, B wait, ch
 // (stored to LDS) at the start of the next iteration before it is re-issued; it issues the same
 // loads in every iteration (clamped addresses), so the compiler's vmcnt bookkeeping stays exact.
 // The other waves issue no global loads inside the passes (the folds only store).
+
+// The loader's B pass (wave kBLoaderWave<ALGO>).
+template <typename T, int ALGO>
+__device__ void bpass_loader(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& dst, const Geom& gm, T* astore,
+                             T* tmstore, int lane, int tl, int nB, unsigned long long* st)
+{
+    (void)st;
+    (void)tmstore;
+    constexpr int kF = kTileDma<T>;
+    // B pass iteration j (wa = tl - j) converts the tiles of wa (tiles tl-2..tl never left the
+    // ring) and tempmax of wa (beta, next iteration) from staging slot j % 3 into the LDS slots
+    // nobody reads this iteration, stages the same streams three windows lower into the slot it
+    // just read, and copies alpha of wa-1 (folded at j+3) straight into LDS slot (wa-1) % 4
+    // (last read at j-1).  All DMAs are unconditional (clamped windows, a spare slot at the
+    // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
+    // own and the previous iteration's DMAs in flight: three windows of latency for each.
+    constexpr int kAd = kDiag<kDiagNoAdma> ? 0 : alpha_dma_count<T, ALGO>();
+    constexpr int kB = kF + 1 + kAd;
+    TD_STAMP(p3);
+    vm_wait<0>();   // the F pass's last (unused) staging
+    if constexpr (ALGO == 0) {
+        // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) converts the tiles of
+        // wa, copies alpha of wa-1 (folded at j+3) into LDS slot (wa-1) % 4 first and stages the
+        // tiles three windows lower, then waits until the previous iteration's alpha copy (window
+        // wa) has landed and forms beta's tempmax of wa from it (tm_from_alpha, beta next
+        // iteration): the copy has one iteration of latency instead of three, the tiles two.
+        // (Issuing the DMAs ahead of the conversion, with a fourth staging slot, measured 0.8 %
+        // slower: the conversion's LDS reads then meet the DMAs' LDS writes.)
+        auto bstep0 = [&](int j, int slot) {
+            TD_STAMP(b0);
+            const int wa = tl - j;
+            if constexpr (!kDiag<kDiagNoBConvert>) {
+                if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+            TD_STAMP(bc);
+            TD_ACC(14, b0, bc);   // stamps build: the loader's slot 14 is its B-pass tile conversion
+            if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+            tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+            TD_STAMP(bw);
+            if (j == 0)
+                vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
+            else
+                vm_wait<kAd + 2 * kF>();   // the previous iteration's alpha copy (window wa) has landed
+            TD_STAMP(bt);
+            TD_ACC(4, bw, bt);   // stamps build: the loader's slot 4 is its B-pass DMA wait
+            if (wa >= 0) tm_from_alpha(sm, wa, lane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            TD_STAMP(b1);
+            TD_ACC(15, bt, b1);   // ... slot 15 its tempmax formation (tm_from_alpha, to its writes' completion)
+            wg_sync_lds();
+            TD_STAMP(b2);
+            TD_ACC(2, b0, b1);
+            TD_ACC(3, b1, b2);
+        };
+        if constexpr (kAd > 0) {
+            alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);      // folded at j = 2
+            alpha_dma_head<T>(sm, astore, gm, tl + 1, lane);   // alpha_raw[.][L] when the last window is full
+        }
+        TD_STAMP(p4);
+        TD_ACC(12, p3, p4);
+        for (int j = 0; j < nB; j += 3) {
+            bstep0(j, 0);
+            if (j + 1 < nB) bstep0(j + 1, 1);
+            if (j + 2 < nB) bstep0(j + 2, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
+        return;
+    }
+    auto bstep = [&](int j, int slot) {
+        TD_STAMP(b0);
+        const int wa = tl - j;
+        if constexpr (!kDiag<kDiagNoBConvert>) {
+            if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
+            if (wa >= 0) tm_convert(sm, slot, wa, lane);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+        tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
+        tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
+        if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
+        TD_STAMP(bw);
+        vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
+        TD_STAMP(b1);
+        TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
+        wg_sync_lds();
+        TD_STAMP(b2);
+        TD_ACC(2, b0, b1);
+        TD_ACC(3, b1, b2);
+    };
+    tile_dma(sm, 0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never converted
+    tm_dma(sm, 0, tmstore, gm, tl, lane);
+    tile_dma(sm, 1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never converted
+    tm_dma(sm, 1, tmstore, gm, tl - 1, lane);
+    tile_dma(sm, 2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never converted
+    tm_dma(sm, 2, tmstore, gm, tl - 2, lane);
+    if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);   // folded at j = 2
+    vm_wait<2 * (kF + 1) + kAd>();   // slot 0 landed
+    TD_STAMP(p4);
+    TD_ACC(12, p3, p4);
+    for (int j = 0; j < nB; j += 3) {
+        bstep(j, 0);
+        if (j + 1 < nB) bstep(j + 1, 1);
+        if (j + 2 < nB) bstep(j + 2, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
+}
 
 // One SISO over the workgroup's 8 codewords.  Each role runs its own loops (so only that role's
 // state is live in its code); every role executes the same sequence of wg_sync_lds barriers:
@@ -1579,8 +1705,12 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         auto fstep = [&](int t) {
             TD_STAMP(f0);
             if (t + 1 <= tl) tile_convert(sm, (t + 1) % 3, src, t + 1, lane);
-            tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
-            vm_wait<kF>();   // window t+2 has landed
+            if (!kFSkip<ALGO> || t + 3 <= tl) {
+                tile_dma(sm, t % 3, src, dst, gm, min(t + 3, tl), lane);
+                vm_wait<kF>();   // window t+2 has landed
+            } else {
+                vm_wait<0>();    // no staging past the last window: nothing is left in flight at the pass end
+            }
             TD_STAMP(f1);
             wg_sync_lds();
             TD_STAMP(f2);
@@ -1599,103 +1729,10 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         TD_STAMP(p1);
         TD_ACC(11, p0, p1);
         for (int t = 0; t < nT; ++t) fstep(t);
-        // B pass iteration j (wa = tl - j) converts the tiles of wa (tiles tl-2..tl never left the
-        // ring) and tempmax of wa (beta, next iteration) from staging slot j % 3 into the LDS slots
-        // nobody reads this iteration, stages the same streams three windows lower into the slot it
-        // just read, and copies alpha of wa-1 (folded at j+3) straight into LDS slot (wa-1) % 4
-        // (last read at j-1).  All DMAs are unconditional (clamped windows, a spare slot at the
-        // tail), so the per-iteration count kB is fixed and every iteration ends leaving only its
-        // own and the previous iteration's DMAs in flight: three windows of latency for each.
-        constexpr int kAd = kDiag<kDiagNoAdma> ? 0 : alpha_dma_count<T, ALGO>();
-        constexpr int kB = kF + 1 + kAd;
-        TD_STAMP(p3);
-        vm_wait<0>();   // the F pass's last (unused) staging
-        if constexpr (ALGO == 0) {
-            // Log-MAP (round 4): no tempmax stream.  Iteration j (wa = tl - j) converts the tiles of
-            // wa, copies alpha of wa-1 (folded at j+3) into LDS slot (wa-1) % 4 first and stages the
-            // tiles three windows lower, then waits until the previous iteration's alpha copy (window
-            // wa) has landed and forms beta's tempmax of wa from it (tm_from_alpha, beta next
-            // iteration): the copy has one iteration of latency instead of three, the tiles two.
-            // (Issuing the DMAs ahead of the conversion, with a fourth staging slot, measured 0.8 %
-            // slower: the conversion's LDS reads then meet the DMAs' LDS writes.)
-            auto bstep0 = [&](int j, int slot) {
-                TD_STAMP(b0);
-                const int wa = tl - j;
-                if constexpr (!kDiag<kDiagNoBConvert>) {
-                    if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
-                TD_STAMP(bc);
-                TD_ACC(14, b0, bc);   // stamps build: the loader's slot 14 is its B-pass tile conversion
-                if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
-                tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
-                TD_STAMP(bw);
-                if (j == 0)
-                    vm_wait<kAd + kF>();       // the prologue's copies (window tl, row L) have landed
-                else
-                    vm_wait<kAd + 2 * kF>();   // the previous iteration's alpha copy (window wa) has landed
-                TD_STAMP(bt);
-                TD_ACC(4, bw, bt);   // stamps build: the loader's slot 4 is its B-pass DMA wait
-                if (wa >= 0) tm_from_alpha(sm, wa, lane);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                TD_STAMP(b1);
-                TD_ACC(15, bt, b1);   // ... slot 15 its tempmax formation (tm_from_alpha, to its writes' completion)
-                wg_sync_lds();
-                TD_STAMP(b2);
-                TD_ACC(2, b0, b1);
-                TD_ACC(3, b1, b2);
-            };
-            if constexpr (kAd > 0) {
-                alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);      // folded at j = 2
-                alpha_dma_head<T>(sm, astore, gm, tl + 1, lane);   // alpha_raw[.][L] when the last window is full
-            }
-            TD_STAMP(p4);
-            TD_ACC(12, p3, p4);
-            for (int j = 0; j < nB; j += 3) {
-                bstep0(j, 0);
-                if (j + 1 < nB) bstep0(j + 1, 1);
-                if (j + 2 < nB) bstep0(j + 2, 2);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
+        if constexpr (kBLoaderWave<ALGO> == 2) {
+            bpass_loader<T, ALGO>(sm, src, dst, gm, astore, tmstore, lane, tl, nB, st);
             return;
         }
-        auto bstep = [&](int j, int slot) {
-            TD_STAMP(b0);
-            const int wa = tl - j;
-            if constexpr (!kDiag<kDiagNoBConvert>) {
-                if (wa >= 0 && wa <= tl - 3) tile_convert(sm, slot, src, wa, lane);
-                if (wa >= 0) tm_convert(sm, slot, wa, lane);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
-            tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
-            tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
-            if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
-            TD_STAMP(bw);
-            vm_wait<2 * kB>();   // everything issued before the previous iteration has landed
-            TD_STAMP(b1);
-            TD_ACC(4, bw, b1);   // stamps build: the loader's slot 4 is its B-pass DMA wait
-            wg_sync_lds();
-            TD_STAMP(b2);
-            TD_ACC(2, b0, b1);
-            TD_ACC(3, b1, b2);
-        };
-        tile_dma(sm, 0, src, dst, gm, max(tl - 3, 0), lane);   // j = 0: never converted
-        tm_dma(sm, 0, tmstore, gm, tl, lane);
-        tile_dma(sm, 1, src, dst, gm, max(tl - 3, 0), lane);   // j = 1: never converted
-        tm_dma(sm, 1, tmstore, gm, tl - 1, lane);
-        tile_dma(sm, 2, src, dst, gm, max(tl - 3, 0), lane);   // j = 2: never converted
-        tm_dma(sm, 2, tmstore, gm, tl - 2, lane);
-        if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, tl, lane);   // folded at j = 2
-        vm_wait<2 * (kF + 1) + kAd>();   // slot 0 landed
-        TD_STAMP(p4);
-        TD_ACC(12, p3, p4);
-        for (int j = 0; j < nB; j += 3) {
-            bstep(j, 0);
-            if (j + 1 < nB) bstep(j + 1, 1);
-            if (j + 2 < nB) bstep(j + 2, 2);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no copy outlives the pass
-        return;
     } else if (dst.sys2_out) {
         // waves 1 and 3, first SISO: SISO2's systematic input sys2[g][i][c] = sys1[g][pi(i)][c]
         // (i < K; :1109-1113), one element of window t per lane (kTile - 64 of 128 lanes in the
@@ -1743,7 +1780,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
     }
 
     // ===================================== B pass (waves 0, 1, 3)
-    if (wave == 1) {
+    if (kBLoaderWave<ALGO> == 3 && wave == 3) {
+        bpass_loader<T, ALGO>(sm, src, dst, gm, astore, tmstore, lane, tl, nB, st);
+    } else if (wave == 1) {
         // beta over window wb = tl - j + 1 (its tempmax was staged last iteration)
         LaneConst<T> lc;
         lane_setup(lt, lane, lc);
