@@ -395,3 +395,49 @@ def test_dropin_latency_driver_matches_reference(tmp_path, name):
     assert rec["frames"] == nf and rec["ms_per_frame"] > 0
     bits = np.fromfile(tmp_path / "bits.bin", dtype=np.uint8).reshape(nf, K)
     assert np.array_equal(bits, d["bits"][:, it - 1])
+
+
+_REDO_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from turbo_decoder_cuda_amd import TurboCodec
+d = np.load(sys.argv[2])
+out = {}
+for prec, dt in (("f64", torch.float64), ("f32", torch.float32)):
+    x = torch.from_numpy(d["flow"]).to("cuda").to(dt).contiguous()
+    K, B, it = int(d["K"]), x.shape[0], int(d["iters"])
+    with TurboCodec(K, int(d["f1"]), int(d["f2"]), iterations=it, precision=prec) as c:
+        bits = torch.empty((B, it, K), dtype=torch.uint8, device=x.device)
+        le = torch.empty((B, it, 2, K + 3), dtype=dt, device=x.device)
+        c.decode(x, bits, all_iters=True, le=le)
+        torch.cuda.synchronize()
+    out["bits_" + prec], out["le_" + prec] = bits.cpu().numpy(), le.cpu().numpy()
+np.savez(sys.argv[3], **out)
+"""
+
+
+def test_alpha_speculation_redo_path_is_exact(tmp_path):
+    """The log-MAP alpha window reads its max* rows speculatively and recomputes a window in the
+    committed order when a bucket check fails (td_kernels.hip kASpec), which practically never
+    happens on real data.  libturbo_mi355x_redo.so (build.py, -DTD_ASPEC_REDO) takes the redo on
+    every window: its bits and Le equal the production library's bit for bit, fp64 and fp32, on
+    the reference's K = 1024 frames and a K = 6144 batch (and the fp64 bits the reference's)."""
+    redo = os.path.join(PKG, "libturbo_mi355x_redo.so")
+    assert os.path.exists(redo), "build() makes the redo-forced library"
+    K, f1, f2 = 6144, 263, 480
+    _, flow = O.synth_batch(K, f1, f2, 0.6, 4242, 11)
+    cases = [("gold", dict(np.load(os.path.join(GOLD, "frames_K1024_e0.5_s11.npz")))),
+             ("k6144", dict(K=K, f1=f1, f2=f2, iters=3, flow=flow))]
+    for tag, d in cases:
+        np.savez(tmp_path / f"{tag}_in.npz", **{k: d[k] for k in ("K", "f1", "f2", "iters", "flow")})
+        env = dict(os.environ, TD_LIB_PATH=redo)
+        subprocess.run(["python", "-c", _REDO_CHILD, REPO, str(tmp_path / f"{tag}_in.npz"), str(tmp_path / f"{tag}_out.npz")],
+                       env=env, check=True, timeout=300)
+        r = np.load(tmp_path / f"{tag}_out.npz")
+        K_, it = int(d["K"]), int(d["iters"])
+        for prec in ("f64", "f32"):
+            bits, le = _decode_all(K_, int(d["f1"]), int(d["f2"]), it, d["flow"].astype(np.float64), precision=prec)
+            assert np.array_equal(r["bits_" + prec], bits), (tag, prec)
+            assert np.array_equal(r["le_" + prec], le), (tag, prec)
+        if tag == "gold":
+            assert np.array_equal(r["bits_f64"], d["bits"])

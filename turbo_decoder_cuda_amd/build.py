@@ -2,6 +2,7 @@
 product is a plain C-ABI shared library (include/turbo_mi355x.h)."""
 from __future__ import annotations
 
+import concurrent.futures
 import os
 import subprocess
 import sys
@@ -61,12 +62,16 @@ def _run_hip(cmd, verbose):
 def build(force: bool = False, verbose: bool = False) -> None:
     srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_kernels_w12.hip", "td_synth.hip", "td_api.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
-    if force or _newer(LIB, deps):
-        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-shared", "-o", LIB, *srcs], verbose)
     stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
-    if force or _newer(stamps, deps):
-        # the same schedule as the production build (the dedicated beta loop fits since round 3)
-        _run_hip([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DTD_STAMPS", "-shared", "-o", stamps, *srcs], False)
+    redo = os.path.join(PKG, "libturbo_mi355x_redo.so")       # test build: every log-MAP alpha window takes
+    jobs = []                                                  # the speculation's exact redo (test_gpu_decode)
+    for out, flags in ((LIB, []), (stamps, ["-DTD_STAMPS"]), (redo, ["-DTD_ASPEC_REDO"])):
+        if force or _newer(out, deps):
+            jobs.append(([HIPCC, f"--offload-arch={ARCH}", *COMMON, *flags, "-shared", "-o", out, *srcs], verbose and out == LIB))
+    # the three builds are independent: run them side by side
+    with concurrent.futures.ThreadPoolExecutor(max_workers=3) as ex:
+        for f in [ex.submit(_run_hip, cmd, v) for cmd, v in jobs]:
+            f.result()
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,

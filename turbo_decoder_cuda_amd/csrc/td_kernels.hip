@@ -1045,14 +1045,62 @@ __device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v)
     gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
 }
 
+// Log-MAP, speculative table row (kASpec): the step's max* row is read from the bucket of the
+// UNnormalised difference fl(fl(g_p + an) - fl(g_s + a)), which is known before the tempmax tree,
+// so the table read (60-70 cycles) overlaps the tree's three (DPP, max) levels and the exact
+// difference's sub / fma / sub instead of following them.  The exact difference d is formed as
+// before and only its bucket is compared with the speculated one (OR-ed into `miss`); the
+// threshold compare, the select and the add use d itself, so a step whose buckets agree is
+// bit-identical to the committed order.  A window with any mismatch in any lane is recomputed in
+// the committed order from its first alpha (alpha_window), stores included, before the barrier:
+// the two differences differ by roundings of the normalisation only, so a mismatch needs d within
+// a few ulps of a bucket edge and the redo practically never runs (TD_ASPEC_REDO forces it on
+// every window: that build must and does decode bit-identically).  One box, 3 interleaved rounds
+// (profiles/r04/ab_v31_aspec.txt): config 2 1502 -> 1521 Mbit/s (+1.3 %), fp32 log-MAP +0.4 %, the
+// 32768 shard level; the fp32 four-per-CU kernel of the 12-step TU lost 3.4 %, so it keeps the
+// committed order.  (With the flag left to the compiler, and with SLP packing the two buckets into
+// 16-bit pairs, the same speculation measured 1.2 % slower.)
+#ifndef TD_ASPEC
+#define TD_ASPEC (TD_KW == 15)
+#endif
+template <typename T, int ALGO>
+constexpr bool kASpec = ALGO == 0 && TD_ASPEC != 0;
+
 template <typename T, int ALGO, int K>
 struct AlphaSchedS {
     static __device__ __forceinline__ void run(T& a, StepIn<T> (&op)[3], const Smem<T>& sm, int tb, const T* lut,
                                                int c, const LaneConst<T>& lc, T* sa, T* stm, const unsigned (&va)[3],
-                                               TmBatch<T>& tbh)
+                                               TmBatch<T>& tbh, unsigned& miss)
     {
         constexpr int PH = K % 3;
         const StepIn<T> in = op[K % 3];
+        if constexpr (kASpec<T, ALGO>) {
+            const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw
+            const T dr = fma(lc.a_pg[PH], in.gp, an) - fma(lc.a_sg[PH], in.gs, a);
+            const int qr = bucket_dev<T>(dr);
+            __builtin_amdgcn_sched_barrier(0);
+            T thr, lo, hi;
+            lut_fields<T>(lut, qr * 2 * kLutCols<T>, thr, lo, hi);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
+            __builtin_amdgcn_sched_barrier(0);
+            astore_row<T, K>(sa, va[PH], a);   // alpha_raw[.][i]
+            __builtin_amdgcn_sched_barrier(0);
+            T m = vmax(a, an);                                   // tempmax[i] (:986-993), alpha_tempmax's tree
+            m = vmax(m, dpp<PhaseDpp<(PH + 1) % 3>::ctrl>(m));
+            m = vmax(m, dpp<PhaseDpp<(PH + 2) % 3>::ctrl>(m));
+            const T alpha = a - m, ap = an - m;                  // :995-1000
+            const T xs = fma(lc.a_sg[PH], in.gs, alpha);
+            const T xp = fma(lc.a_pg[PH], in.gp, ap);
+            const T d = xp - xs;
+            // per step, in a VGPR (left to itself the compiler turns the flag into 15 compares and
+            // SALU ORs of VCC at the window's end, on the chain's tail)
+            unsigned x = (unsigned)bucket_dev<T>(d);
+            asm("v_xor_b32 %1, %1, %2\n\tv_or_b32 %0, %0, %1" : "+v"(miss), "+v"(x) : "v"(qr));
+            a = sched_finish(xs, xp, d, thr, lo, hi);
+            AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh, miss);
+            return;
+        }
         T an;                                         // partner's alpha_raw
         const T m = alpha_tempmax<T, PH>(a, an);       // tempmax[i] (:986-993)
         const T alpha = a - m, ap = an - m;                   // :995-1000
@@ -1080,13 +1128,13 @@ struct AlphaSchedS {
             __builtin_amdgcn_sched_barrier(0);
             a = vmax(xs, xp);
         }
-        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh);
+        AlphaSchedS<T, ALGO, K + 1>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh, miss);
     }
 };
 template <typename T, int ALGO>
 struct AlphaSchedS<T, ALGO, kW> {
     static __device__ __forceinline__ void run(T&, StepIn<T> (&)[3], const Smem<T>&, int, const T*, int,
-                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], TmBatch<T>&)
+                                               const LaneConst<T>&, T*, T*, const unsigned (&)[3], TmBatch<T>&, unsigned&)
     {
     }
 };
@@ -1661,7 +1709,17 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
                     op[1] = alpha_in<T, 1>(sm, tb, 1, c, lc);
                     __builtin_amdgcn_sched_barrier(0);   // the window's first reads issue first
                     TD_CHAIN_T0(c0);
-                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh);
+                    const T a0 = a;
+                    unsigned miss = 0;
+                    AlphaSchedS<T, ALGO, 0>::run(a, op, sm, tb, lut, c, lc, sa, stm, va, tbh, miss);
+                    if constexpr (kASpec<T, ALGO>) {
+#ifdef TD_ASPEC_REDO
+                        miss = 1;
+#endif
+                        if (__builtin_amdgcn_ballot_w64(miss != 0))   // a bucket mismatch: the window again, committed order
+                            a = alpha_window<T, ALGO>(a0, t, kW, sm, lut, c, lc, ga0 + (size_t)t * aws,
+                                                      gtm0 + (size_t)t * kW * kCw);
+                    }
                     TD_CHAIN_ACC(c0);
                     sa += aws;
                     stm += (size_t)kW * kCw;
