@@ -292,3 +292,17 @@ def test_placement_stop_rule_min_candidates(ms, stop, monkeypatch):
     monkeypatch.delenv("TD_PLACEMENT_MIN", raising=False)
     arr = (C.c_float * len(ms))(*ms)
     assert N.lib().td_debug_placement_rule(arr, len(ms)) == stop
+
+
+@pytest.mark.parametrize("name", ["libturbo_mi355x_redo.so", "libturbo_mi355x_stamps.so"])
+def test_test_builds_load_and_export_the_abi(name):
+    """build() also makes the redo-forced build (tests/test_gpu_decode.py, the α speculation's exact
+    redo on every window) and the stamps build (scripts/diag_stamps.py): both load without a GPU and
+    export every declared entry point, so a TD_LIB_PATH swap is a drop-in (checked in a child
+    process: one process, one copy of the HIP runtime's kernel registrations)."""
+    path = os.path.join(PKG, name)
+    assert os.path.exists(path), f"build() makes {name}"
+    code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); "
+            "missing = [s for s in sys.argv[2:] if not hasattr(L, s)]; print(missing); sys.exit(1 if missing else 0)")
+    r = subprocess.run(["python", "-c", code, path, *declared_functions()], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
