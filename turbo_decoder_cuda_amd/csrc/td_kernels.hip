@@ -1520,13 +1520,10 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 #ifndef TD_BLOADER_MAX
 #define TD_BLOADER_MAX 3
 #endif
-#ifndef TD_FSKIP
-#define TD_FSKIP 0
-#endif
 template <int ALGO>
 constexpr int kBLoaderWave = ALGO == 1 ? TD_BLOADER_MAX : TD_BLOADER_LOG;
 template <int ALGO>
-constexpr bool kFSkip = TD_FSKIP != 0 || kBLoaderWave<ALGO> == 3;
+constexpr bool kFSkip = kBLoaderWave<ALGO> == 3;   // (on its own, with F0 loading both passes: level)
 static_assert(TD_BLOADER_LOG == 2 || TD_BLOADER_LOG == 3, "B-pass loader: wave 2 or 3");
 static_assert(TD_BLOADER_MAX == 2 || TD_BLOADER_MAX == 3, "B-pass loader: wave 2 or 3");
 constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
