@@ -167,12 +167,16 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
 
+    power = PowerSampler(local) if rank == 0 else None
     codec.profile(True)   # hipEvents around each kernel, inside the timed region
+    if power is not None:
+        power.start()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         codec.decode(llr, bits, stream=stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    power_rec = power.stop() if power is not None else None
     barrier()
     demux_ms, turbo_ms, nlaunch = codec.kernel_ms()
     codec.profile(False)
@@ -191,6 +195,7 @@ def main():
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
     out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock)
     out["workspace_placement"] = placement_record(placement, turbo_ms, a.iters)
+    out["power"] = power_rec
 
     if rank == 0 and world == 1 and not a.no_variants:
         out["pcie_inclusive"] = pcie_inclusive(a, codec, llr, dev, stream)
@@ -206,6 +211,70 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class PowerSampler:
+    """Board power and shader clock of this rank's GPU (amdsmi), sampled every ~10 ms from a host
+    thread while the timed region runs.  The config-2 launch sits at the board's power limit
+    (1360-1378 W at 2.27-2.30 GHz), so the record says which cap a box's clock met.
+    Monitoring only: any amdsmi failure leaves the record null and the bench unchanged."""
+
+    def __init__(self, device: int):
+        self.h, self.samples, self.limit = None, [], None
+        try:
+            import amdsmi
+            import torch
+            amdsmi.amdsmi_init()
+            self.smi = amdsmi
+            hs = amdsmi.amdsmi_get_processor_handles()
+            prop = torch.cuda.get_device_properties(device)
+            bus = getattr(prop, "pci_bus_id", None)
+            for h in hs:   # the torch device's PCI bus; a single visible GPU otherwise
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)
+                if bus is not None and int(bdf.split(":")[1], 16) == int(bus):
+                    self.h = h
+            if self.h is None and len(hs) == 1:
+                self.h = hs[0]
+            if self.h is not None:
+                lim = amdsmi.amdsmi_get_power_info(self.h).get("power_limit")
+                self.limit = lim if isinstance(lim, (int, float)) else None
+        except Exception:
+            self.h = None
+
+    def _read(self):
+        p = self.smi.amdsmi_get_power_info(self.h).get("current_socket_power")
+        c = self.smi.amdsmi_get_clock_info(self.h, self.smi.AmdSmiClkType.SYS).get("clk")
+        return (float(p) if isinstance(p, (int, float)) else None, float(c) if isinstance(c, (int, float)) else None)
+
+    def start(self):
+        import threading
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                try:
+                    self.samples.append(self._read())
+                except Exception:
+                    return
+                self._stop.wait(0.01)
+        if self.h is not None:
+            self._t = threading.Thread(target=loop, daemon=True)
+            self._t.start()
+        return self
+
+    def stop(self):
+        if self.h is None:
+            return None
+        self._stop.set()
+        self._t.join(timeout=2.0)
+        pw = [p for p, _ in self.samples if p is not None]
+        ck = [c for _, c in self.samples if c is not None]
+        if not pw:
+            return None
+        return {"socket_w_mean": round(sum(pw) / len(pw), 1), "socket_w_max": max(pw),
+                "sclk_mhz_mean": round(sum(ck) / len(ck), 1) if ck else None, "samples": len(pw),
+                "power_limit_w": self.limit, "source": "amdsmi current_socket_power / SYS clock, ~10 ms apart, timed region",
+                "note": "the launch is board-power-capped (DESIGN.md 5): the clock a box reaches at this limit sets its speed"}
 
 
 def placement_record(placement, turbo_ms: float, iters: int) -> dict:

@@ -92,3 +92,11 @@ def test_traffic_model_matches_the_pmc_total():
     m = bench.traffic_model(6144, 4096, 8, 8, "logmap", 15, alpha_raw=not pmc["kernel"].startswith("v29"))
     assert abs(m["total"] / pmc["bytes_per_launch"] - 1) < 0.02
     assert max(m["bytes"], key=m["bytes"].get) == "alpha"
+
+
+def test_power_sampler_is_inert_without_a_gpu():
+    """bench.PowerSampler (board power / clock record of the timed region) never fails a bench:
+    with no GPU (or no amdsmi) its record is null."""
+    import bench
+    s = bench.PowerSampler(0).start()
+    assert s.stop() is None
