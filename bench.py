@@ -237,7 +237,8 @@ class PowerSampler:
                 self.h = hs[0]
             if self.h is not None:
                 lim = amdsmi.amdsmi_get_power_info(self.h).get("power_limit")
-                self.limit = lim if isinstance(lim, (int, float)) else None
+                # amdsmi reports the limit in microwatts (1400000000 on MI355X), the socket power in W
+                self.limit = (lim / 1e6 if lim > 1e5 else lim) if isinstance(lim, (int, float)) else None
         except Exception:
             self.h = None
 
