@@ -300,6 +300,15 @@ constexpr int kWaves = kGroupWaves;                  // waves per codeword group
 // 12-step windows (round 3).
 constexpr int kFoldA = kTile / 2;
 static_assert(kFoldA <= kLanes && kTile - kFoldA <= kLanes, "one fold item per lane");
+// fp64 Max-Log-MAP, whose B pass the two fold waves (A and F0) bound: A takes 64 items (8 whole
+// steps), F0 the other 56 (profiles/r04/ab_v32_maxlog_foldsplit.txt: config 3 +1.2 %, its 32768
+// batch +1.5 %; 56/64 the same; fp32 Max-Log-MAP lost 1.5 % either way and keeps 60/60).
+#ifndef TD_FOLDA_MAX
+#define TD_FOLDA_MAX 64
+#endif
+template <typename T, int ALGO>
+constexpr int kFoldAOf = (ALGO == 1 && sizeof(T) == 8) ? TD_FOLDA_MAX : kFoldA;   // items of fold wave A
+static_assert(kFoldAOf<double, 1> <= kLanes && kTile - kFoldAOf<double, 1> <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 // every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
 template <int ALGO>
@@ -1889,8 +1898,9 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
         }
     } else {
         // waves 0 and 3: fold window wf = tl - j + 2, one item per lane
-        int fe = (wave == 0 ? 0 : kFoldA) + lane;
-        int nfold = wave == 0 ? kFoldA : kTile - kFoldA;
+        constexpr int kFA = kFoldAOf<T, ALGO>;
+        int fe = (wave == 0 ? 0 : kFA) + lane;
+        int nfold = wave == 0 ? kFA : kTile - kFA;
         if constexpr (!kFoldRows<ALGO> && kTile - kTile / 3 <= kLanes) {
             // (kW = 12 only: with 15-step windows the other two phases hold 80 items, more than a wave.)
             // Items by recompute depth when alpha rows are not all kept: wave A (beside the loader)
