@@ -268,6 +268,10 @@ class PowerSampler:
             return None
         self._stop.set()
         self._t.join(timeout=2.0)
+        try:
+            self.smi.amdsmi_shut_down()
+        except Exception:
+            pass
         pw = [p for p, _ in self.samples if p is not None]
         ck = [c for _, c in self.samples if c is not None]
         if not pw:
