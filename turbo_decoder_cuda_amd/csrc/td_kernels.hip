@@ -121,6 +121,13 @@ struct PhaseDpp {
     static constexpr int ctrl = PH == 0 ? kDppXor1 : (PH == 1 ? kDppXor2 : kDppMir8);
 };
 
+// x + s*g for a sign s = +-1 and a DPP-moved x: fma(s, g, x), exact.  fp32 writes it as a multiply
+// (off the chain) and an add whose DPP operand the compiler folds into v_add_f32_dpp, so the move
+// leaves the chain; fp64 has no 64-bit DPP operand and keeps the fma (its code is unchanged).
+// fp32 log-MAP +2.0 %, Max-Log-MAP and the 32768 batch level (profiles/r04/ab_v33_f32_partner_add_dpp.txt).
+__device__ __forceinline__ double fma_pm(double s, double g, double x) { return fma(s, g, x); }
+__device__ __forceinline__ float fma_pm(float s, float g, float x) { return x + s * g; }
+
 // fmax -> v_max_f64 / v_max_f32.  Equal to the reference's `x > y ? x : y` / running
 // `if (m < a) m = a` for every non-NaN pair (they can differ only in the sign of a zero,
 // which never changes a later non-zero value or a hard decision).
@@ -916,7 +923,7 @@ template <typename T, int ALGO, int PH>
 __device__ __forceinline__ T beta_step(T beta, const StepIn<T>& in, const T* lut, const LaneConst<T>& lc)
 {
     const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
-    const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], in.gs, beta), fma(lc.b_pg[PH], in.gp, bp), lut);
+    const T b = mstar<T, ALGO>(fma(lc.b_sg[PH], in.gs, beta), fma_pm(lc.b_pg[PH], in.gp, bp), lut);
     return b - in.tm;
 }
 
@@ -928,7 +935,7 @@ __device__ __forceinline__ StepHalf<T> beta_issue(T beta, const StepIn<T>& in, c
     const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
     StepHalf<T> h;
     h.xs = fma(lc.b_sg[PH], in.gs, beta);
-    h.xp = fma(lc.b_pg[PH], in.gp, bp);
+    h.xp = fma_pm(lc.b_pg[PH], in.gp, bp);
     if constexpr (ALGO == 0) {
         h.d = h.xp - h.xs;
         const LutRow r = lut_row(h.d);
@@ -1089,7 +1096,7 @@ struct AlphaSchedS {
         const StepIn<T> in = op[K % 3];
         if constexpr (kASpec<T, ALGO>) {
             const T an = dpp<PhaseDpp<PH>::ctrl>(a);   // partner's alpha_raw
-            const T dr = fma(lc.a_pg[PH], in.gp, an) - fma(lc.a_sg[PH], in.gs, a);
+            const T dr = fma_pm(lc.a_pg[PH], in.gp, an) - fma(lc.a_sg[PH], in.gs, a);
             const int qr = bucket_dev<T>(dr);
             __builtin_amdgcn_sched_barrier(0);
             T thr, lo, hi;
@@ -1169,7 +1176,7 @@ struct BetaSched {
         bs[K] = beta;
         const T bp = dpp<PhaseDpp<PH>::ctrl>(beta);
         const T xs = fma(lc.b_sg[PH], in.gs, beta);
-        const T xp = fma(lc.b_pg[PH], in.gp, bp);
+        const T xp = fma_pm(lc.b_pg[PH], in.gp, bp);
         const T d = xp - xs;
         const LutRow r = lut_row(d);
         __builtin_amdgcn_sched_barrier(0);
