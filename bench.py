@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--window", type=int, default=0, help="0 = exact schedule; 64 = sliding window (config 5)")
     ap.add_argument("--overlap", type=int, default=30, help="sliding-window warm-up steps")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-power", action="store_true",
+                    help="no amdsmi sampling thread in the timed region (A/B of its cost: DESIGN.md 5)")
     ap.add_argument("--dropin-frames", type=int, default=8,
                     help="frames for the drop-in per-frame latency (0 = skip; N=1, fp64 log-MAP only)")
     return ap.parse_args(argv)
@@ -154,6 +156,7 @@ def main():
         codec.set_window(a.window, a.overlap)
     codec.reserve(a.batch)   # also picks the workspace placement (td_reserve)
     placement = codec.placement()
+    placement_cost = codec.placement_cost()
     bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -167,7 +170,7 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
 
-    power = PowerSampler(local) if rank == 0 else None
+    power = PowerSampler(local) if rank == 0 and not a.no_power else None
     codec.profile(True)   # hipEvents around each kernel, inside the timed region
     if power is not None:
         power.start()
@@ -194,7 +197,7 @@ def main():
         np.save(os.path.join(a.dump_bits, f"bits_rank{rank}_first{first}.npy"), bits.cpu().numpy())
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
     out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock)
-    out["workspace_placement"] = placement_record(placement, turbo_ms, a.iters)
+    out["workspace_placement"] = placement_record(placement, turbo_ms, a.iters, placement_cost)
     out["power"] = power_rec
 
     if rank == 0 and world == 1 and not a.no_variants:
@@ -203,7 +206,8 @@ def main():
         n = min(a.cpu_sample, a.batch)
         out["cpu_baseline"] = cpu_baseline(a, llr64[:n].cpu().numpy(), bits[:n].cpu().numpy(), f1, f2)
     if rank == 0 and world == 1 and a.dropin_frames > 0 and not a.window and a.precision == "f64" and a.algo == "logmap":
-        out["dropin"] = dropin(a, llr64[: a.dropin_frames].cpu().numpy(), f1, f2, local)
+        out["dropin"] = dropin(a, llr64[: a.dropin_frames].cpu().numpy(), f1, f2, local,
+                               info=u_d[: a.dropin_frames].cpu().numpy())
     if rank == 0 and world == 1 and not a.no_variants:
         out["variants"] = variants(a, codec, llr64, u_d, f1, f2, dev, stream)
         out["demod"] = demod_rates(a, dev)
@@ -220,12 +224,12 @@ class PowerSampler:
     Monitoring only: any amdsmi failure leaves the record null and the bench unchanged."""
 
     def __init__(self, device: int):
-        self.h, self.samples, self.limit = None, [], None
+        self.h, self.samples, self.limit, self.smi = None, [], None, None
         try:
             import amdsmi
             import torch
             amdsmi.amdsmi_init()
-            self.smi = amdsmi
+            self.smi = amdsmi   # initialised: shut down in stop() / close() on every path
             hs = amdsmi.amdsmi_get_processor_handles()
             prop = torch.cuda.get_device_properties(device)
             bus = getattr(prop, "pci_bus_id", None)
@@ -241,6 +245,17 @@ class PowerSampler:
                 self.limit = (lim / 1e6 if lim > 1e5 else lim) if isinstance(lim, (int, float)) else None
         except Exception:
             self.h = None
+        if self.h is None:
+            self.close()
+
+    def close(self):
+        """amdsmi_shut_down once, whenever amdsmi_init succeeded."""
+        if self.smi is not None:
+            try:
+                self.smi.amdsmi_shut_down()
+            except Exception:
+                pass
+            self.smi = None
 
     def _read(self):
         p = self.smi.amdsmi_get_power_info(self.h).get("current_socket_power")
@@ -264,14 +279,13 @@ class PowerSampler:
         return self
 
     def stop(self):
-        if self.h is None:
-            return None
-        self._stop.set()
-        self._t.join(timeout=2.0)
         try:
-            self.smi.amdsmi_shut_down()
-        except Exception:
-            pass
+            if self.h is None:
+                return None
+            self._stop.set()
+            self._t.join(timeout=2.0)
+        finally:
+            self.close()
         pw = [p for p, _ in self.samples if p is not None]
         ck = [c for _, c in self.samples if c is not None]
         if not pw:
@@ -282,13 +296,16 @@ class PowerSampler:
                 "note": "the launch is board-power-capped (DESIGN.md 5): the clock a box reaches at this limit sets its speed"}
 
 
-def placement_record(placement, turbo_ms: float, iters: int) -> dict:
+def placement_record(placement, turbo_ms: float, iters: int, cost=None) -> dict:
     """td_reserve's workspace placement search beside the full launch it chose for: the kept
     candidate's one-iteration probe time x iterations is what the probe predicts for a launch, so a
     'fast probe, slow launch' box shows as launch_over_probe well above 1."""
     ms, kept = placement
     rec = {"probe_ms": ms, "kept": kept,
            "note": "one-iteration probe per candidate workspace at td_reserve (outside the timed region)"}
+    if cost and cost[0] is not None and ms:
+        rec["search_wall_ms"] = round(cost[0], 1)
+        rec["search_peak_gib_held"] = round(cost[1] / 2**30, 2)
     if ms and 0 <= kept < len(ms):
         rec["kept_probe_ms"] = ms[kept]
         rec["probe_x_iters_ms"] = round(ms[kept] * iters, 4)
@@ -300,12 +317,18 @@ def placement_record(placement, turbo_ms: float, iters: int) -> dict:
 DROPIN = os.path.join(REPO, "turbo_decoder_cuda_amd", "td_dropin_latency")
 
 
-def dropin(a, flows, f1, f2, device: int) -> dict:
+DROPIN_WINDOW = {"TD_WINDOW": "64", "TD_OVERLAP": "30"}   # the opt-in low-latency schedule (config 5's)
+
+
+def dropin(a, flows, f1, f2, device: int, info=None) -> dict:
     """The unchanged reference caller's per-frame latency (ITTC/main.cpp:221: one TurboDecoding per
     frame, 15 iterations = N_ITERATION): examples/dropin_latency.cpp linked against
     libturbo_logmap_compat.so, a child process on this GPU, warm handle after its first frame.  Beside
     it the compiled reference's TurboDecoding loop on one host core at 15 iterations, per frame.
-    Bits: the drop-in's last-iteration rows against the reference's on the same frames."""
+    Bits: the drop-in's last-iteration rows against the reference's on the same frames.
+    `window`: the same caller with the compat layer's opt-in sub-block schedule (TD_WINDOW=64,
+    TD_OVERLAP=30, read at TurboCodingInit): its per-frame time and its bits against the exact
+    schedule's and the source bits (BER-gated, not bit-exact)."""
     import subprocess
     import tempfile
 
@@ -314,17 +337,39 @@ def dropin(a, flows, f1, f2, device: int) -> dict:
     if not os.access(DROPIN, os.X_OK):
         rec["error"] = "td_dropin_latency not built"
         return rec
-    env = dict(os.environ, TD_ITERATIONS="15", TD_DEVICE=str(device))
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "flows.bin"), os.path.join(td, "bits.bin")
         np.ascontiguousarray(flows, dtype=np.float64).tofile(fin)
-        r = subprocess.run([DROPIN, str(a.K), str(f1), str(f2), str(n), fin, fout], capture_output=True, text=True,
-                           env=env, timeout=300)
-        if r.returncode:
-            rec["error"] = (r.stdout + r.stderr)[-400:]
+
+        def run(extra):
+            env = dict(os.environ, TD_ITERATIONS="15", TD_DEVICE=str(device), **extra)
+            for k in DROPIN_WINDOW:
+                if k not in extra:
+                    env.pop(k, None)
+            r = subprocess.run([DROPIN, str(a.K), str(f1), str(f2), str(n), fin, fout], capture_output=True,
+                               text=True, env=env, timeout=300)
+            if r.returncode:
+                return None, (r.stdout + r.stderr)[-400:]
+            return (json.loads(r.stdout.strip().splitlines()[-1]),
+                    np.fromfile(fout, dtype=np.uint8).reshape(n, a.K)), None
+
+        res, err = run({})
+        if err:
+            rec["error"] = err
             return rec
-        rec.update(json.loads(r.stdout.strip().splitlines()[-1]))
-        gpu_bits = np.fromfile(fout, dtype=np.uint8).reshape(n, a.K)
+        rec.update(res[0])
+        gpu_bits = res[1]
+        wres, werr = run(DROPIN_WINDOW)
+        if werr:
+            rec["window"] = {"error": werr}
+        else:
+            w = {"env": dict(DROPIN_WINDOW), "ms_per_frame": wres[0]["ms_per_frame"], "ms_first": wres[0]["ms_first"],
+                 "ms_min": wres[0]["ms_min"], "speedup_vs_exact": round(rec["ms_per_frame"] / wres[0]["ms_per_frame"], 3),
+                 "bits_differing_from_exact": int((wres[1] != gpu_bits).sum())}
+            if info is not None:
+                w["bit_errors"] = int((wres[1] != info).sum())
+                rec["bit_errors"] = int((gpu_bits != info).sum())
+            rec["window"] = w
         if os.access(REF_HARNESS, os.X_OK):
             nr = min(n, 4)
             rout = os.path.join(td, "rbits.bin")
@@ -337,9 +382,11 @@ def dropin(a, flows, f1, f2, device: int) -> dict:
             rec["reference"] = f"the compiled reference (ITTC/log_map.cpp, g++ -O2), one host core, {nr} frames"
             rec["bits_match_reference"] = bool(np.array_equal(gpu_bits[:nr], ref_bits))
             rec["speedup_vs_reference"] = round(rec["reference_ms_per_frame"] / rec["ms_per_frame"], 3)
+            if isinstance(rec.get("window"), dict) and "ms_per_frame" in rec["window"]:
+                rec["window"]["speedup_vs_reference"] = round(rec["reference_ms_per_frame"] / rec["window"]["ms_per_frame"], 3)
     rec["note"] = ("per-frame latency of the batch-of-one path: one codeword group on one CU, so the time is "
                    "the serial alpha / beta chains of 30 SISOs (DESIGN.md 5); throughput callers batch "
-                   "(td_decode_device), the headline value")
+                   "(td_decode_device), the headline value; `window` is the opt-in sub-block schedule")
     return rec
 
 
@@ -400,31 +447,47 @@ def traffic_model(K: int, B: int, iters: int, esz: int, algo: str, W: int = 15, 
             "scratch_share": round((alpha + tm) / total, 4), "window_steps": W}
 
 
-# Dependent-chain cycles per trellis step of the two recursions, each alone on a SIMD with its
-# operands in registers (scripts/ubench_alpha.hip, scripts/ubench_beta.hip): fp64
-# log-MAP alpha 200 (218 with its two scratch stores), beta 148.
-CHAIN_CYCLES_F64_LOGMAP = {"alpha": 218, "beta": 148}
+# Dependent-chain cycles per trellis step of the two recursions (fp64 log-MAP):
+#   isolated   each alone on a SIMD with its operands in registers (scripts/ubench_alpha.hip,
+#              scripts/ubench_beta.hip): alpha 218 with its two scratch stores (committed order), beta 148;
+#   in_kernel  the chains' own loops inside the production schedule, from the stamps build
+#              (profiles/r04/stamps_v31_aspec.txt, slot 4 of waves A and B): alpha 182 (the speculative
+#              table-row read of round 4, stores in its shadow), beta 153 (its LDS reads beside the folds).
+# The floor is priced at the in-kernel figures (the isolated alpha overstated the
+# fraction); the isolated floor rides along.
+CHAIN_CYCLES_F64_LOGMAP = {"alpha": 182, "beta": 153}
+CHAIN_CYCLES_F64_LOGMAP_ISOLATED = {"alpha": 218, "beta": 148}
 SCLK_GHZ = 2.35   # fallback only: the sustained shader clock measured on earlier boxes
 
 
 def latency_floor(a, turbo_ms, sclk_ghz=None):
     """The exact schedule's own speed of light: every codeword of a dispatch round is in flight at
     once, so a launch cannot beat 2*iters SISOs x L steps x (alpha step + beta step), the two serial
-    recursions back to back, at the chains' isolated per-step latency, at the launch's own measured
-    shader clock (td_clock_read).  frac = floor / measured."""
+    recursions back to back, at the chains' in-kernel per-step latency, at the launch's own measured
+    shader clock (td_clock_read).  frac = floor / measured.  The rest of the launch is the schedule's
+    overhead around the chains (window starts, barrier waits, SISO prologues: DESIGN.md 8.5)."""
     if a.window or a.algo != "logmap" or a.precision != "f64" or turbo_ms <= 0:
         return None
     clk = sclk_ghz if sclk_ghz else SCLK_GHZ
     rounds = -(-((a.batch + 7) // 8) // 512)   # dispatch rounds of 512 workgroups (2 per CU)
-    cyc = CHAIN_CYCLES_F64_LOGMAP["alpha"] + CHAIN_CYCLES_F64_LOGMAP["beta"]
-    floor_ms = rounds * 2 * a.iters * (a.K + 3) * cyc / (clk * 1e9) * 1e3
+
+    def floor(c):
+        return rounds * 2 * a.iters * (a.K + 3) * (c["alpha"] + c["beta"]) / (clk * 1e9) * 1e3
+
+    floor_ms, iso_ms = floor(CHAIN_CYCLES_F64_LOGMAP), floor(CHAIN_CYCLES_F64_LOGMAP_ISOLATED)
+    per_step = turbo_ms * 1e-3 * clk * 1e9 / (rounds * 2 * a.iters * (a.K + 3))
     return {"floor_ms": round(floor_ms, 3), "frac": round(floor_ms / turbo_ms, 4),
-            "chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP, "sclk_ghz": round(clk, 4),
+            "chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP, "chain_source": "in-kernel (stamps build)",
+            "isolated": {"chain_cycles_per_step": CHAIN_CYCLES_F64_LOGMAP_ISOLATED, "floor_ms": round(iso_ms, 3),
+                         "frac": round(iso_ms / turbo_ms, 4)},
+            "launch_cycles_per_step": round(per_step, 1),
+            "overhead_cycles_per_step": round(per_step - sum(CHAIN_CYCLES_F64_LOGMAP.values()), 1),
+            "sclk_ghz": round(clk, 4),
             "sclk_source": "measured (td_clock_read)" if sclk_ghz else "constant (no clock sample)",
             "dispatch_rounds": rounds,
-            "note": "serial alpha + beta chains at their isolated per-step latency (microbenchmarks), "
-                    "the bound this latency-limited kernel is measured against; the HBM fraction above "
-                    "is the metric's contract"}
+            "note": "serial alpha + beta chains at their in-kernel per-step latency, the bound this "
+                    "latency-limited kernel is measured against; the overhead is itemised in DESIGN.md 8.5; "
+                    "the HBM fraction above is the metric's contract"}
 
 
 def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock=None) -> dict:

@@ -72,7 +72,7 @@ int td_reserve(td_handle* h, int B);
  * stops once one candidate runs >= 4 % below the median of those timed, never on a slow
  * straggler.  Transient memory: every candidate is
  * held until the choice (so each gets fresh pages), at most half the free device memory and at
- * most 144 GiB in total (config 2: ~2.4 GiB a candidate; a 32768-codeword batch: ~19 GiB).
+ * most 64 GiB in total (config 2: ~2.6 GB a candidate; a 32768-codeword batch: ~21 GiB, three).
  * Results do not depend on it.
  * Occupancy: a decode of more than 512 groups of 8 codewords (B > 4096 on 256 CUs) in fp32 runs
  * three or four workgroups per CU instead of two where that finishes sooner (fp32 log-MAP 1.5x,
@@ -131,8 +131,9 @@ int td_profile_enable(td_handle* h, int on);
 int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches);
 /* Launch clock (measurement support): every exact-schedule turbo launch records, in its first
  * workgroup, the shader clock (s_memtime) and the 100 MHz real-time counter (s_memrealtime) at that
- * workgroup's start and end.  td_clock_read synchronises the device and returns the last launch's
- * sustained shader clock (GHz) and the workgroup's span (ms); TD_EINVAL before any such launch. */
+ * workgroup's start and end.  td_clock_read waits for this handle's last decode (not the whole
+ * device) and returns that launch's sustained shader clock (GHz) and the workgroup's span (ms);
+ * TD_EINVAL before any such launch or when the last decode was windowed or graph-captured. */
 int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms);
 
 /* Diagnostics: in a library built with -DTD_STAMPS (td_debug_stamp_slots() > 0) the turbo
@@ -144,6 +145,8 @@ int td_debug_stamp_slots(void);
  * candidate workspaces timed (0 = plain allocation), their probe times in ms (up to cap of them)
  * and the index kept. */
 int td_debug_placement(td_handle* h, float* ms, int cap, int* pick);
+/* Cost of that search: its wall time (ms) and the peak bytes of candidate workspaces it held. */
+int td_debug_placement_cost(td_handle* h, double* wall_ms, double* held_bytes);
 /* The placement search's stop rule on probe times ms[0..n) (host only, for tests): 1 if the search
  * would stop after them (the fast mode seen), else 0; TD_EINVAL on a bad argument. */
 int td_debug_placement_rule(const float* ms, int n);

@@ -64,6 +64,10 @@ def lib():
         L.tdo_siso_f32.argtypes = [C.POINTER(Trellis), P, P, C.c_int, P, C.c_int, C.c_int]
         L.tdo_turbo_decode_f64.argtypes = [C.POINTER(Trellis), P, P, C.c_int, C.c_int, C.c_int, P, P]
         L.tdo_turbo_decode_f32.argtypes = [C.POINTER(Trellis), P, P, C.c_int, C.c_int, C.c_int, P, P]
+        for sfx in ("f64", "f32"):
+            getattr(L, f"tdo_turbo_decode_window_{sfx}").argtypes = [C.POINTER(Trellis), P, P, C.c_int, C.c_int,
+                                                                    C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                                    C.c_int, C.c_double, P, P]
         L.tdo_decode_batch.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int, P, C.c_int]
         L.tdo_synth_batch.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_uint64, C.c_int, P, P]
         L.tdo_glibc_srand.argtypes = [C.POINTER(GlibcRand), C.c_uint]
@@ -137,6 +141,25 @@ def turbo_decode(flow: np.ndarray, K: int, f1: int, f2: int, iters: int, algo: i
     fn = lib().tdo_turbo_decode_f32 if f32 else lib().tdo_turbo_decode_f64
     fn(C.byref(t), _p(pi), _p(flow), K, iters, algo, _p(bits), _p(le))
     return bits, le
+
+
+def turbo_decode_window(flow: np.ndarray, K: int, f1: int, f2: int, iters: int, W: int, g: int,
+                       algo: int = ALGO_LOGMAP, nii: bool = False, concurrent: bool = False, scale: float = 1.0,
+                       nrm: int | None = None):
+    """One codeword through the sub-block schedule restatement (turbo_oracle_window.inc): the
+    arithmetic of the HIP windowed kernel, normalised every nrm positions of a sub-block (default:
+    the kernel's checkpoint spacing, 4 in fp64, 8 in fp32).  Returns (bits[iters,K] uint8, le[iters,2,L])."""
+    f32 = flow.dtype == np.float32
+    flow = np.ascontiguousarray(flow)
+    L = K + 3
+    bits = np.zeros((iters, K), dtype=np.int32)
+    le = np.zeros((iters, 2, L), dtype=flow.dtype)
+    t = trellis()
+    pi = qpp(K, f1, f2)
+    nrm = nrm or (8 if f32 else 4)
+    fn = lib().tdo_turbo_decode_window_f32 if f32 else lib().tdo_turbo_decode_window_f64
+    fn(C.byref(t), _p(pi), _p(flow), K, iters, algo, W, g, nrm, int(nii), int(concurrent), scale, _p(bits), _p(le))
+    return bits.astype(np.uint8), le
 
 
 def decode_batch(flow: np.ndarray, K: int, f1: int, f2: int, iters: int, algo: int = ALGO_LOGMAP,

@@ -380,6 +380,7 @@ void tdo_demultiplex(const double* flow, int K, const int* pi, double* yk) { dem
 #define SFX f64
 #define MAXSTAR(x, y) tdo_maxstar((x), (y))
 #include "turbo_oracle_siso.inc"
+#include "turbo_oracle_window.inc"
 #undef REAL
 #undef SFX
 #undef MAXSTAR
@@ -388,6 +389,7 @@ void tdo_demultiplex(const double* flow, int K, const int* pi, double* yk) { dem
 #define SFX f32
 #define MAXSTAR(x, y) tdo_maxstar_f32((x), (y))
 #include "turbo_oracle_siso.inc"
+#include "turbo_oracle_window.inc"
 #undef REAL
 #undef SFX
 #undef MAXSTAR

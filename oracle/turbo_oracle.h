@@ -106,6 +106,26 @@ void tdo_turbo_decode_f32(const tdo_trellis* t, const int* pi, const float* flow
                           int algo, int* out, float* le_dump);
 
 /*
+ * The sub-block (sliding-window) schedule of td_set_window (BASELINE config 5), restated on
+ * log_map.cpp's arithmetic (turbo_oracle_window.inc has the definition and the citations):
+ * sub-blocks of W steps, overlap g, chains normalised every nrm positions of their sub-block
+ * (the HIP kernel's checkpoint spacing: 4 fp64, 8 fp32), NII boundaries, serial or concurrent
+ * SISOs, extrinsic scale.  Same outputs as tdo_turbo_decode_*.
+ */
+void tdo_turbo_decode_window_f64(const tdo_trellis* t, const int* pi, const double* flow, int K, int iters,
+                                 int algo, int W, int g, int nrm, int nii, int concurrent, double scale,
+                                 int* out, double* le_dump);
+void tdo_turbo_decode_window_f32(const tdo_trellis* t, const int* pi, const float* flow, int K, int iters,
+                                 int algo, int W, int g, int nrm, int nii, int concurrent, double scale,
+                                 int* out, float* le_dump);
+void tdo_window_siso_f64(const tdo_trellis* t, const double* ys, const double* yp, const double* La, int L, int W,
+                         int g, int nrm, int algo, int use_nii, const double* nii_a, const double* nii_b,
+                         double* new_a, double* new_b, double* LLR);
+void tdo_window_siso_f32(const tdo_trellis* t, const float* ys, const float* yp, const float* La, int L, int W,
+                         int g, int nrm, int algo, int use_nii, const float* nii_a, const float* nii_b,
+                         float* new_a, float* new_b, float* LLR);
+
+/*
  * Batch front-end used for the CPU baseline and the parity tests: B codewords, each flow row
  * of 3K+12 values (f64 or f32 by `f32`), nthreads host threads (codewords dealt round-robin).
  * bits[B][K] = final-iteration hard bits (uint8).  Returns 0.

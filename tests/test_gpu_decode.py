@@ -311,6 +311,32 @@ def test_compat_turbo_decoding(driver, tmp_path, name):
     assert np.array_equal(flow2, d["flow"] * 0.5)
 
 
+@pytest.mark.parametrize("algo,W,g", [("maxlog", 16, 48), ("logmap", 64, 30), ("logmap", 32, 30)])
+def test_compat_window_schedule(driver, tmp_path, algo, W, g):
+    """The compat layer's opt-in sub-block schedule (TD_WINDOW / TD_OVERLAP, read at
+    TurboCodingInit): the unchanged caller's TurboDecoding then runs the windowed kernels.  Its rows
+    equal the windowed restatement (oracle/turbo_oracle_window.inc) bit for bit; with Max-Log-MAP
+    and an overlap reaching both trellis ends (K = 40: L = 43 <= 48) they also equal the exact
+    decoder's (the exact anchor of test_gpu_window.py).  Without TD_WINDOW the same driver is the
+    exact schedule (test_compat_turbo_decoding)."""
+    K, f1, f2, nf, it = (40, 3, 10, 4, 4) if algo == "maxlog" else (1024, 31, 64, 3, 4)
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 51 + W, nf)
+    flow.astype(np.float64).tofile(tmp_path / "flow.bin")
+    env = dict(os.environ, TD_ITERATIONS=str(it), TD_WINDOW=str(W), TD_OVERLAP=str(g), TD_ALGO=algo)
+    subprocess.run([driver, "decode", str(K), str(f1), str(f2), str(nf), str(tmp_path / "flow.bin"),
+                    str(tmp_path / "out.bin")], env=env, timeout=300, check=True)
+    out = np.fromfile(tmp_path / "out.bin", dtype=np.int32).reshape(nf, 15, K)[:, :it].astype(np.uint8)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(nf):
+        wb, _ = O.turbo_decode_window(flow[b], K, f1, f2, it, W, g, algo=oalgo)
+        assert np.array_equal(out[b], wb), f"frame {b}"
+        if algo == "maxlog":
+            ob, _ = O.turbo_decode(flow[b], K, f1, f2, it, algo=oalgo)
+            assert np.array_equal(out[b], ob.astype(np.uint8)), f"frame {b}"
+    flow2 = np.fromfile(str(tmp_path / "out.bin") + ".flow", dtype=np.float64).reshape(nf, -1)
+    assert np.array_equal(flow2, flow * 0.5)
+
+
 def test_decode_rejects_bad_buffers():
     """Shape / dtype / device checks of TurboCodec.decode (the kernels would write past a short
     buffer): wrong stream length, all_iters bits of the final-only shape, Le of the other dtype."""

@@ -9,6 +9,11 @@ pin the kernel's indexing first:
 and every schedule option (sub-block length, overlap, NII boundaries, concurrent SISOs, extrinsic
 scale) is checked in Max-Log-MAP against oracle/window_oracle.py, a restatement of the
 reference's sub-block GPU decoder (ITTC/CUDA/turboDecoderBianJieZhi.cu).
+Since round 5 every schedule, in log-MAP and Max-Log-MAP, fp64 and fp32, in both lane layouts
+(one sub-block per lane; runs of consecutive sub-blocks per lane, forced by TD_WINDOW_RUN), is
+compared bit for bit with oracle/turbo_oracle_window.inc (pyoracle.turbo_decode_window), the C
+restatement of the windowed kernels' arithmetic, which tests/test_window_oracle.py pins to the
+numpy restatement above and to the exact oracle.
 Then the BER of the windowed log-MAP decoder at K=6144 is compared with the exact schedule on
 the same generator frames."""
 import numpy as np
@@ -66,6 +71,55 @@ def test_window_schedules_vs_restatement(K, f1, f2, W, g, nii, conc, scale):
         ob, ol = WO.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, nii=nii, concurrent=conc, scale=scale)
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
         assert np.array_equal(bits[b], ob), f"codeword {b}"
+
+
+# (K, f1, f2, W, g, nii, concurrent, scale, TD_WINDOW_RUN): run 0 = the layout's own choice (one
+# sub-block per lane at these batches); runs need g <= W and W a multiple of the checkpoint spacing
+WIN_CASES = [
+    (1024, 31, 64, 64, 30, False, False, 1.0, 0),
+    (1024, 31, 64, 64, 30, False, False, 1.0, 2),
+    (1024, 31, 64, 64, 30, True, False, 1.0, 5),      # 16 sub-blocks in runs of 5 (the last run 1)
+    (512, 31, 64, 48, 48, True, True, 0.77, 3),       # overlap = window
+    (200, 13, 50, 48, 0, True, True, 0.77, 2),        # the reference GPU decoder's schedule, in runs
+    (200, 13, 50, 64, 0, True, False, 1.0, 3),
+    (200, 13, 50, 50, 9, True, True, 0.77, 2),        # W not a multiple of 4: one sub-block per lane
+    (160, 21, 120, 64, 192, True, True, 1.0, 2),      # overlap beyond both ends: one per lane
+    (40, 3, 10, 16, 0, True, True, 0.5, 2),
+    (6144, 263, 480, 64, 30, False, False, 1.0, 7),   # config 5's schedule, 96 sub-blocks in runs of 7
+]
+
+
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("K,f1,f2,W,g,nii,conc,scale,run", WIN_CASES)
+def test_window_vs_c_restatement(monkeypatch, K, f1, f2, W, g, nii, conc, scale, run, algo):
+    """Every schedule option, both algorithms, both lane layouts: bits identical to the C
+    restatement, Le within 1e-9 (the same fp64 operations in the same order)."""
+    monkeypatch.setenv("TD_WINDOW_RUN", str(run))
+    B, iters = (3, 3) if K > 2048 else (9, 5)
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 11 + W + g, B)
+    bits, le = _decode(K, f1, f2, iters, flow, algo, W, g, ext_scale=scale, nii=nii, concurrent=conc)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(B):
+        ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo, nii=nii, concurrent=conc,
+                                       scale=scale)
+        assert np.array_equal(bits[b], ob), f"codeword {b}"
+        assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
+
+
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("run", [0, 3])
+def test_window_f32_vs_c_restatement(monkeypatch, algo, run):
+    """fp32 (checkpoints and normalisation every 8 positions) against the fp32 restatement."""
+    monkeypatch.setenv("TD_WINDOW_RUN", str(run))
+    K, f1, f2, B, iters, W, g = 1024, 31, 64, 9, 4, 64, 30
+    _, flow = O.synth_batch(K, f1, f2, 0.5, 77, B)
+    flow = flow.astype(np.float32)
+    bits, le = _decode(K, f1, f2, iters, flow, algo, W, g, precision="f32")
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(B):
+        ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo)
+        assert np.array_equal(bits[b], ob), f"codeword {b}"
+        assert np.abs(le[b] - ol).max() <= 1e-4 * max(1.0, np.abs(ol).max()), f"codeword {b}"
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -177,3 +231,20 @@ def test_config5_full_batch():
         ob, ol = WO.turbo_decode_window(fs[k], K, f1, f2, iters, 64, 30)
         assert np.array_equal(bs[k], ob), f"codeword {sample[k]}"
         assert np.abs(ls[k] - ol).max() <= 1e-9, f"codeword {sample[k]}"
+    # the bench's config-5 line itself (fp64 log-MAP, the run layout this batch selects): two seeded
+    # codewords equal to the C restatement in every iteration's bits, Le within 1e-9
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.synth_seed(20261015)
+        _, llr = c.synth(B, 1.0)
+        c.set_window(64, 30, 1.0)
+        c.reserve(B)
+        bits = torch.empty((B, iters, K), dtype=torch.uint8, device=llr.device)
+        le = torch.empty((B, iters, 2, K + 3), dtype=torch.float64, device=llr.device)
+        c.decode(llr, bits, all_iters=True, le=le)
+        torch.cuda.synchronize()
+        bs, ls, fs = bits[idx].cpu().numpy(), le[idx].cpu().numpy(), llr[idx].cpu().numpy()
+    del bits, le, llr
+    for k in range(len(sample)):
+        ob, ol = O.turbo_decode_window(fs[k], K, f1, f2, iters, 64, 30)
+        assert np.array_equal(bs[k], ob), f"codeword {sample[k]} (log-MAP)"
+        assert np.abs(ls[k] - ol).max() <= 1e-9, f"codeword {sample[k]} (log-MAP)"

@@ -22,7 +22,7 @@ EXPORTS = (
     "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read", "td_debug_set_stamps",
     "td_debug_stamp_slots", "td_synth_seed", "td_synth_frames", "td_count_errors", "td_rand_window", "td_synth_seek",
     "td_set_window", "td_synth_modulation", "td_modulate", "td_demodulate", "td_debug_placement",
-    "td_debug_placement_rule", "td_clock_read", "td_window_steps",
+    "td_debug_placement_rule", "td_clock_read", "td_window_steps", "td_debug_placement_cost",
 )
 
 
@@ -81,6 +81,8 @@ def lib() -> C.CDLL:
     L.td_debug_stamp_slots.restype = I
     L.td_debug_placement.argtypes = [P, C.POINTER(C.c_float), I, C.POINTER(C.c_int)]
     L.td_debug_placement_rule.argtypes = [C.POINTER(C.c_float), I]
+    if hasattr(L, "td_debug_placement_cost"):   # (older A/B builds loaded by TD_LIB_PATH lack it)
+        L.td_debug_placement_cost.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.td_profile_read.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
     if hasattr(L, "td_clock_read"):   # measurement support (older A/B builds loaded by TD_LIB_PATH lack it)
         L.td_clock_read.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]

@@ -59,17 +59,33 @@ def _run_hip(cmd, verbose):
         raise RuntimeError("kernels use scratch: " + ", ".join(bad))
 
 
-def build(force: bool = False, verbose: bool = False) -> None:
+def _workers(n: int) -> int:
+    """Parallel hipcc jobs: each whole-kernel compile takes a few GB; keep to the memory at hand."""
+    try:
+        avail = os.sysconf("SC_AVPHYS_PAGES") * os.sysconf("SC_PAGE_SIZE") / 2**30
+    except (ValueError, OSError):
+        avail = 8.0
+    return max(1, min(n, int(avail // 6)))
+
+
+def build(force: bool = False, verbose: bool = False, extra: bool = True) -> None:
+    """The product library, the compat layer and the drop-in driver.  extra: also the two test /
+    diagnostic builds of the same sources (libturbo_mi355x_redo.so, which every log-MAP alpha window
+    takes the speculation's exact redo in, for test_alpha_speculation_redo_path_is_exact; and the
+    stamps build for scripts/diag_stamps.py).  __graft_entry__.build() asks for them, as the GPU
+    tests load the redo build."""
     srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_kernels_w12.hip", "td_synth.hip", "td_api.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
     stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
     redo = os.path.join(PKG, "libturbo_mi355x_redo.so")       # test build: every log-MAP alpha window takes
     jobs = []                                                  # the speculation's exact redo (test_gpu_decode)
     for out, flags in ((LIB, []), (stamps, ["-DTD_STAMPS"]), (redo, ["-DTD_ASPEC_REDO"])):
+        if out != LIB and not extra:
+            continue
         if force or _newer(out, deps):
             jobs.append(([HIPCC, f"--offload-arch={ARCH}", *COMMON, *flags, "-shared", "-o", out, *srcs], verbose and out == LIB))
-    # the three builds are independent: run them side by side
-    with concurrent.futures.ThreadPoolExecutor(max_workers=3) as ex:
+    # the builds are independent: run them side by side, as memory allows
+    with concurrent.futures.ThreadPoolExecutor(max_workers=_workers(len(jobs) or 1)) as ex:
         for f in [ex.submit(_run_hip, cmd, v) for cmd, v in jobs]:
             f.result()
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
@@ -84,4 +100,4 @@ def build(force: bool = False, verbose: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose="-v" in sys.argv)
+    build(force="--force" in sys.argv, verbose="-v" in sys.argv, extra="--no-extra" not in sys.argv)

@@ -15,8 +15,16 @@
 //     out[N_ITERATION*K], one row of hard bits per iteration (:1261-1264);
 //   * failures print a message and exit(1), as the reference does (:288-292, 357-368);
 //   * AWGN draws its seed from the process's rand() exactly like the reference.
-// Environment: TD_DEVICE (HIP ordinal, default 0), TD_ITERATIONS (default 15 = N_ITERATION),
-// TD_ALGO ("logmap" | "maxlog").
+// Environment, read when the handle opens (TurboCodingInit, or a new K): TD_DEVICE (HIP ordinal,
+// default 0), TD_ITERATIONS (default 15 = N_ITERATION), TD_ALGO ("logmap" | "maxlog").
+// Opt-in low-latency schedule (default: the exact schedule, bit-exact with log_map.cpp):
+//   TD_WINDOW=W     sub-blocks of W trellis steps decoded in parallel (td_set_window); the frame's
+//                   time is then one sub-block's chains instead of the whole trellis's
+//   TD_OVERLAP=g    warm-up steps of each sub-block's alpha / beta (default min(30, 3W))
+//   TD_NII=1        boundary metrics from the previous iteration
+//   TD_CONCURRENT=1 both SISOs at once (Jacobi); TD_EXT_SCALE=s extrinsic scale (default 1)
+// A windowed schedule changes the arithmetic (sub-block boundaries): its results are gated by
+// the BER curve, not bit-exact.  Log_MAP_decoder always runs the exact SISO.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +54,27 @@ int env_int(const char* name, int dflt)
     return v && *v ? std::atoi(v) : dflt;
 }
 
+double env_double(const char* name, double dflt)
+{
+    const char* v = std::getenv(name);
+    return v && *v ? std::atof(v) : dflt;
+}
+
+// TD_WINDOW & co. (see the file header): the exact schedule unless TD_WINDOW is set and non-zero
+void set_schedule(td_handle* h)
+{
+    const int W = env_int("TD_WINDOW", 0);
+    if (W == 0) return;
+    td_window_params w{};
+    w.window = W;
+    w.overlap = env_int("TD_OVERLAP", W > 0 && 3 * W < 30 ? 3 * W : 30);
+    w.nii = env_int("TD_NII", 0);
+    w.concurrent = env_int("TD_CONCURRENT", 0);
+    w.ext_scale = env_double("TD_EXT_SCALE", 1.0);
+    const int rc = td_set_window(h, &w);
+    if (rc) die("td_set_window (TD_WINDOW / TD_OVERLAP / TD_EXT_SCALE)", rc);
+}
+
 void open_handle(int K)
 {
     if (g_h && g_K == K) return;
@@ -62,6 +91,7 @@ void open_handle(int K)
     p.device = env_int("TD_DEVICE", 0);
     const int rc = td_create(&g_h, &p);
     if (rc) die("td_create", rc);
+    set_schedule(g_h);
     g_K = K;
 }
 

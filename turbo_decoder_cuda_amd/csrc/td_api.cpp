@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -61,6 +62,7 @@ struct td_handle {
     td::LaneTables* d_lane = nullptr;
     unsigned* d_slots = nullptr;   // per-CU occupancy bits of the turbo kernel (wg_pos)
     unsigned long long* d_clk = nullptr;   // the last exact-schedule launch's clock samples (td_clock_read)
+    bool clk_exact = false;                // the last decode was an exact-schedule launch (d_clk is its sample)
     // td_decode_host's device staging (input stream, bits, optional Le), grown on demand and kept: the
     // drop-in's TurboDecoding decodes one frame per call, so per-call allocations would be per frame
     void* d_hin = nullptr;
@@ -71,6 +73,7 @@ struct td_handle {
     void* d_ws = nullptr;   // decode workspace
     std::vector<float> place_ms;   // td_reserve's placement trials (ms of one probe iteration each)
     int place_pick = -1;
+    double place_wall_ms = 0, place_held = 0;   // the search's wall time and peak bytes held
     size_t ws_bytes = 0;
     int ws_groups = 0;
     size_t elem = 8;
@@ -90,7 +93,7 @@ struct td_handle {
     int role_cus = 0;                            // CU count for the kernel's role rotation (wg_pos)
     int occ3 = 1;                                // TD_OCC3=0: never three workgroups per CU
     // decoding schedule (td_set_window): window 0 = exact full trellis
-    td::WindowParams wp{0, 0, 0, 0, 1.0f};
+    td::WindowParams wp{0, 0, 0, 0, 1.0, 0};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
     // Workspace ordering across streams: every decode uses the same d_ws / d_wws, so a decode
@@ -100,9 +103,6 @@ struct td_handle {
     hipEvent_t ws_free = nullptr;   // recorded after the last decode's kernels
     hipStream_t ws_stream = nullptr;
     bool ws_pending = false;
-#ifdef TD_WS_EXPERIMENT
-    char* ovr[8] = {};   // diagnostics: workspace arrays taken from another handle (td_debug_swap_arrays)
-#endif
 };
 
 namespace td {
@@ -168,17 +168,21 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     dp.cu_slots = h->d_slots;
 }
 
-// Workspace carve for G groups of the handle's K.
+// Workspace carve for G groups of the handle's K.  The alpha scratch (astore) belongs to the exact
+// schedule only, the tempmax stream (tmstore) to its Max-Log-MAP form only (log-MAP forms tempmax on
+// chip since round 4); the windowed schedule uses neither (its buffers: win_carve).  An absent region
+// has size 0 (its pointer stays inside the allocation and is never dereferenced).
 struct Carve {
     size_t sys1, par1, sys2, par2, ext12, ext21, astore, tmstore, total;
 };
 
-Carve carve(int G, int K, size_t elem)
+Carve carve(int G, int K, size_t elem, int algo, bool exact)
 {
     const int L = K + td::kMemory;
     const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
     const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
-    const size_t arrA = align_up(td::astore_elems(G, L) * elem, 256);
+    const size_t arrA = exact ? align_up(td::astore_elems(G, L) * elem, 256) : 0;
+    const size_t arrT = exact && algo == TD_ALGO_MAXLOG ? arrL : 0;
     Carve c{};
     c.sys1 = 0;
     c.par1 = c.sys1 + arrL;
@@ -188,104 +192,32 @@ Carve carve(int G, int K, size_t elem)
     c.ext21 = c.ext12 + arrK;
     c.astore = c.ext21 + arrK;
     c.tmstore = c.astore + arrA;
-    c.total = c.tmstore + arrL;
-#ifdef TD_WS_EXPERIMENT   // diagnostics build: gaps (env, bytes) before astore, tmstore and ext12
-    auto gap = [](const char* n) { const char* e = std::getenv(n); return e ? (size_t)std::strtoull(e, nullptr, 0) & ~(size_t)255 : 0; };
-    const size_t ge = gap("TD_WS_GAP_E"), ga = gap("TD_WS_GAP_A"), gt = gap("TD_WS_GAP_T");
-    c.ext12 += ge; c.ext21 += ge; c.astore += ge + ga; c.tmstore += ge + ga + gt; c.total += ge + ga + gt;
-#endif
+    c.total = c.tmstore + arrT;
     return c;
 }
+Carve carve_for(const td_handle* h, int G) { return carve(G, h->p.K, h->elem, h->p.algo, h->wp.window == 0); }
 
-// Workspace allocations.  TD_WS_VMM builds (diagnostics) map the workspace through the virtual
-// memory API instead: physical chunks of TD_VMM_CHUNK bytes (environment; 0 = one chunk) from
-// hipMemCreate, mapped into one reserved range -- to see whether the placement modes follow the
-// page / fragment size behind the workspace.
-#ifdef TD_WS_VMM
-struct VmmRec {
-    void* ptr;
-    size_t size;
-    std::vector<hipMemGenericAllocationHandle_t> chunks;
-};
-std::vector<VmmRec> g_vmm;
-hipError_t ws_malloc(void** p, size_t size)
-{
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = dev;
-    size_t gran = 0;
-    e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
-    if (e != hipSuccess) return e;
-    size_t chunk = 0;
-    if (const char* c = std::getenv("TD_VMM_CHUNK")) chunk = std::strtoull(c, nullptr, 0);
-    size = align_up(size, gran);
-    chunk = chunk ? align_up(chunk, gran) : size;
-    VmmRec r{nullptr, size, {}};
-    e = hipMemAddressReserve(&r.ptr, size, std::max(gran, (size_t)2 << 20), nullptr, 0);
-    if (e != hipSuccess) return e;
-    for (size_t o = 0; o < size; o += chunk) {
-        const size_t n = std::min(chunk, size - o);
-        hipMemGenericAllocationHandle_t hd;
-        e = hipMemCreate(&hd, n, &prop, 0);
-        if (e != hipSuccess) return e;
-        r.chunks.push_back(hd);
-        e = hipMemMap(static_cast<char*>(r.ptr) + o, n, 0, hd, 0);
-        if (e != hipSuccess) return e;
-    }
-    hipMemAccessDesc acc{};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(r.ptr, size, &acc, 1);
-    if (e != hipSuccess) return e;
-    std::fprintf(stderr, "td: VMM workspace %zu B in %zu chunk(s), granularity %zu\n", size, r.chunks.size(), gran);
-    *p = r.ptr;
-    g_vmm.push_back(std::move(r));
-    return hipSuccess;
-}
-hipError_t ws_release(void* p)
-{
-    for (size_t i = 0; i < g_vmm.size(); ++i)
-        if (g_vmm[i].ptr == p) {
-            (void)hipDeviceSynchronize();
-            (void)hipMemUnmap(p, g_vmm[i].size);
-            for (auto hd : g_vmm[i].chunks) (void)hipMemRelease(hd);
-            (void)hipMemAddressFree(p, g_vmm[i].size);
-            g_vmm.erase(g_vmm.begin() + i);
-            return hipSuccess;
-        }
-    return hipFree(p);
-}
-#else
 hipError_t ws_malloc(void** p, size_t size) { return hipMalloc(p, size); }
 hipError_t ws_release(void* p) { return hipFree(p); }
-#endif
 
+// the workspace for G groups in the handle's current layout (grown, never shrunk; ws_groups = the
+// exact-schedule groups it was placed for by td_reserve's search, 0 after a plain growth)
 int ensure_ws(td_handle* h, int G)
 {
-    if (G <= h->ws_groups) return TD_OK;
-    const Carve c = carve(G, h->p.K, h->elem);
+    const Carve c = carve_for(h, G);
+    if (c.total <= h->ws_bytes) return TD_OK;
     if (h->d_ws) {
         TD_HIP(hipDeviceSynchronize());
         TD_HIP(ws_release(h->d_ws));
         h->d_ws = nullptr;
         h->ws_groups = 0;
     }
-#if defined(TD_WS_EXPERIMENT) && defined(TD_WS_CONTIG)   // diagnostics: physically contiguous, slack for the gaps / offset
-    if (hipExtMallocWithFlags(&h->d_ws, c.total + (512u << 20), hipDeviceMallocContiguous) != hipSuccess) {
-#elif defined(TD_WS_EXPERIMENT)
-    if (hipMalloc(&h->d_ws, c.total + (512u << 20)) != hipSuccess) {
-#else
     if (ws_malloc(&h->d_ws, c.total) != hipSuccess) {
-#endif
         h->d_ws = nullptr;
         return fail(TD_ENOMEM, "hipMalloc of the decode workspace failed (" + std::to_string(c.total) + " B)");
     }
     h->ws_bytes = c.total;
-    h->ws_groups = G;
+    h->ws_groups = 0;
     return TD_OK;
 }
 
@@ -304,7 +236,7 @@ int ensure_ws(td_handle* h, int G)
 template <typename T>
 float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e0, hipEvent_t e1, int warm)
 {
-    const Carve c = carve(G, h->p.K, sizeof(T));
+    const Carve c = carve(G, h->p.K, sizeof(T), h->p.algo, true);
     td::DecodeParams<T> dp{};
     fill_common(dp, h);
     dp.sys1 = reinterpret_cast<T*>(ws + c.sys1);
@@ -375,11 +307,11 @@ bool placement_fast_seen(const std::vector<float>& ms)
 }
 
 // Candidate workspaces the search may hold at once: half the free device memory, and at most
-// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  144 GiB
-// lets config 4's 32768-codeword shard (19 GiB a workspace) try seven candidates: with two (the
-// 48 GiB cap of round 3's first runs) both landed in the slow mode (18.96 / 18.58 ms probes), and
-// at N = 8 the slowest of eight ranks sets the step time, so every rank should find the fast mode.
-constexpr size_t kPlaceHoldBytes = (size_t)144 << 30;
+// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  Round 5: 64
+// GiB (was 144): config 2 (2.6 GB a workspace) still probes up to 24 candidates,
+// config 4's 32768-codeword shard (21 GiB without the round-4 tempmax region) three instead of
+// seven.  The search's wall time and peak bytes held are recorded (td_debug_placement_cost).
+constexpr size_t kPlaceHoldBytes = (size_t)64 << 30;
 
 int place_ws(td_handle* h, int G)
 {
@@ -392,7 +324,7 @@ int place_ws(td_handle* h, int G)
         h->d_ws = nullptr;
         h->ws_groups = 0;
     }
-    const Carve c = carve(G, h->p.K, h->elem);
+    const Carve c = carve_for(h, G);
     // every HIP object of the search is released on every exit path, error returns included
     struct Search {
         hipStream_t st = nullptr;
@@ -408,6 +340,7 @@ int place_ws(td_handle* h, int G)
             if (st) (void)hipStreamDestroy(st);
         }
     } s;
+    const auto t_start = std::chrono::steady_clock::now();
     TD_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
     TD_HIP(hipEventCreate(&s.e0));
     TD_HIP(hipEventCreate(&s.e1));
@@ -434,6 +367,8 @@ int place_ws(td_handle* h, int G)
         if (s.cand[i].first < s.cand[best].first) best = i;
     h->place_ms = ms_all;
     h->place_pick = (int)best;
+    h->place_held = (double)s.cand.size() * (double)c.total;
+    h->place_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     h->d_ws = s.cand[best].second;
     s.cand[best].second = nullptr;   // kept; the guard frees the others
     h->ws_bytes = c.total;
@@ -447,7 +382,7 @@ int groups_for(int B) { return (B + 7) / 8; }   // groups of 8 codewords, one wo
 // schedule), the alpha checkpoints of each decoder and the NII metrics [2 parity][2 dec][B][nS][2][8],
 // grown on demand
 struct WinCarve {
-    size_t arrK, arrC, nii, total;
+    size_t arrK, arrC, nii, arrT, total;
 };
 WinCarve win_carve(const td_handle* h, int B)
 {
@@ -457,7 +392,9 @@ WinCarve win_carve(const td_handle* h, int B)
     c.arrK = align_up((size_t)G * K * 8 * elem, 256);
     c.nii = (size_t)2 * 2 * B * td::window_subblocks(L, h->wp.window) * 16 * elem;
     c.arrC = align_up(td::window_ckpt_elems(B, L, h->wp.window, elem == 4) * elem, 256);
-    c.total = 2 * c.arrK + 2 * c.arrC + c.nii;
+    c.nii = align_up(c.nii, 256);
+    c.arrT = align_up(td::window_bits_bytes(B, K), 256);
+    c.total = 2 * c.arrK + 2 * c.arrC + c.nii + c.arrT;
     return c;
 }
 
@@ -496,6 +433,7 @@ int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& 
     wb.ckpt[0] = reinterpret_cast<T*>(w + 2 * arrK);
     wb.ckpt[1] = reinterpret_cast<T*>(w + 2 * arrK + arrC);   // the concurrent SISOs run together
     wb.nii = reinterpret_cast<T*>(w + 2 * arrK + 2 * arrC);
+    wb.bitsT = reinterpret_cast<uint8_t*>(w + 2 * arrK + 2 * arrC + c.nii);
     return TD_OK;
 }
 
@@ -506,11 +444,8 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     const int G = groups_for(B);
     int rc = ensure_ws(h, G);
     if (rc) return rc;
-    const Carve c = carve(G, h->p.K, sizeof(T));
+    const Carve c = carve_for(h, G);
     char* ws = static_cast<char*>(h->d_ws);
-#ifdef TD_WS_EXPERIMENT   // diagnostics build: the carve starts TD_WS_OFFSET bytes into the workspace
-    if (const char* o = std::getenv("TD_WS_OFFSET")) ws += std::strtoull(o, nullptr, 0) & ~(size_t)255;
-#endif
     td::DecodeParams<T> dp{};
     fill_common(dp, h);
     dp.sys1 = reinterpret_cast<T*>(ws + c.sys1);
@@ -521,13 +456,6 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.ext21 = reinterpret_cast<T*>(ws + c.ext21);
     dp.astore = reinterpret_cast<T*>(ws + c.astore);
     dp.tmstore = reinterpret_cast<T*>(ws + c.tmstore);
-#ifdef TD_WS_EXPERIMENT
-    {
-        T** arr[8] = {&dp.sys1, &dp.par1, &dp.sys2, &dp.par2, &dp.ext12, &dp.ext21, &dp.astore, &dp.tmstore};
-        for (int i = 0; i < 8; ++i)
-            if (h->ovr[i]) *arr[i] = reinterpret_cast<T*>(h->ovr[i]);
-    }
-#endif
     dp.llr_out = nullptr;
     dp.pi = h->d_pi;
     dp.pinv = h->d_pinv;
@@ -577,6 +505,7 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     else
         e = td::launch_turbo<T>(dp, st);
     if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
+    h->clk_exact = !h->wp.window && !capturing;
     if (ev) {
         TD_HIP(hipEventRecord(ev[2], st));
         ++h->nev;
@@ -889,7 +818,7 @@ int td_set_window(td_handle* h, const td_window_params* w)
 {
     if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
     if (!w || w->window == 0) {
-        h->wp = td::WindowParams{0, 0, 0, 0, 1.0f};
+        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0};
         return TD_OK;
     }
     if (w->window < 3 || w->window > 10000) return fail(TD_EINVAL, "td_set_window: window must be 0 or in [3, 10000]");
@@ -897,7 +826,11 @@ int td_set_window(td_handle* h, const td_window_params* w)
         return fail(TD_EINVAL, "td_set_window: overlap must be in [0, 3*window]");
     if (!(w->ext_scale > 0.0) || !(w->ext_scale <= 4.0))
         return fail(TD_EINVAL, "td_set_window: ext_scale must be in (0, 4]");
-    h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale};
+    // TD_WINDOW_RUN (environment, tests): sub-blocks per lane run, forcing the run layout on batches too
+    // small to choose it (the results do not depend on it)
+    const char* run = std::getenv("TD_WINDOW_RUN");
+    h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale,
+                             run ? std::atoi(run) : 0};
     return TD_OK;
 }
 
@@ -933,8 +866,9 @@ int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launch
 int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms)
 {
     if (!h) return fail(TD_EINVAL, "td_clock_read: null handle");
+    if (!h->clk_exact) return fail(TD_EINVAL, "td_clock_read: the last decode was not an exact-schedule launch");
     TD_HIP(hipSetDevice(h->p.device));
-    TD_HIP(hipDeviceSynchronize());
+    if (h->ws_pending && h->ws_free) TD_HIP(hipEventSynchronize(h->ws_free));   // this handle's last decode only
     unsigned long long v[4] = {};
     TD_HIP(hipMemcpy(v, h->d_clk, sizeof v, hipMemcpyDeviceToHost));
     const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);   // s_memrealtime: 100 MHz
@@ -960,49 +894,13 @@ int td_debug_placement(td_handle* h, float* ms, int cap, int* pick)
     return n;
 }
 
-#ifdef TD_WS_EXPERIMENT
-// Diagnostics build only (not in the header): the workspace allocation and the byte offset of the
-// alpha scratch inside it (scripts/ws_copy_probe.py streams through it to time plain copies).
-int td_debug_ws(td_handle* h, void** ptr, size_t* bytes, size_t* astore_off)
+int td_debug_placement_cost(td_handle* h, double* wall_ms, double* held_bytes)
 {
-    if (!h || !h->d_ws) return fail(TD_EINVAL, "td_debug_ws: no workspace");
-    const Carve c = carve(h->ws_groups, h->p.K, h->elem);
-    *ptr = h->d_ws;
-    *bytes = h->ws_bytes;
-    *astore_off = c.astore;
+    if (!h) return fail(TD_EINVAL, "td_debug_placement_cost: null handle");
+    if (wall_ms) *wall_ms = h->place_wall_ms;
+    if (held_bytes) *held_bytes = h->place_held;
     return TD_OK;
 }
-
-// Diagnostics build only (not in the header): swap workspace arrays between two handles of the same
-// K, precision and reserved batch, to find which array carries the placement mode.
-// mask bits 0-7: sys1 par1 sys2 par2 ext12 ext21 astore tmstore; bit 8: pi + pinv; bit 9: the
-// max* table, lane tables and CU slot words.  Swapping twice restores both handles.
-int td_debug_swap_arrays(td_handle* a, td_handle* b, int mask)
-{
-    if (!a || !b || a->p.K != b->p.K || a->elem != b->elem || a->ws_groups != b->ws_groups || !a->d_ws || !b->d_ws)
-        return fail(TD_EINVAL, "td_debug_swap_arrays: handles differ");
-    TD_HIP(hipDeviceSynchronize());
-    const Carve c = carve(a->ws_groups, a->p.K, a->elem);
-    const size_t off[8] = {c.sys1, c.par1, c.sys2, c.par2, c.ext12, c.ext21, c.astore, c.tmstore};
-    for (int i = 0; i < 8; ++i)
-        if ((mask >> i) & 1) {
-            char* ea = a->ovr[i] ? a->ovr[i] : static_cast<char*>(a->d_ws) + off[i];
-            char* eb = b->ovr[i] ? b->ovr[i] : static_cast<char*>(b->d_ws) + off[i];
-            a->ovr[i] = eb;
-            b->ovr[i] = ea;
-        }
-    if ((mask >> 8) & 1) {
-        std::swap(a->d_pi, b->d_pi);
-        std::swap(a->d_pinv, b->d_pinv);
-    }
-    if ((mask >> 9) & 1) {
-        std::swap(a->d_lut, b->d_lut);
-        std::swap(a->d_lane, b->d_lane);
-        std::swap(a->d_slots, b->d_slots);
-    }
-    return TD_OK;
-}
-#endif
 
 int td_debug_placement_rule(const float* ms, int n)
 {

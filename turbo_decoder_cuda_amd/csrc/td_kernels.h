@@ -55,8 +55,10 @@ struct DecodeParams {
     T* par2;   // [G][L][8] parity 2
     T* ext12;  // [G][K][8] Le of decoder 1 scattered to interleaved order (= La of decoder 2)
     T* ext21;  // [G][K][8] Le of decoder 2 scattered to natural order (= La of decoder 1)
-    T* astore;    // alpha[.][i] by 8c + state (F pass -> B pass scratch), [G][L][64] (astore_elems)
-    T* tmstore;   // [G][L][8] tempmax[i+1] per step and codeword
+    T* astore;    // F pass -> B pass scratch by 8c + state, [G][L+1][64] (astore_elems): log-MAP alpha_raw of
+                  // rows 0..L; Max-Log-MAP the normalised alpha of the rows i = 0 mod 3
+    T* tmstore;   // [G][L][8] tempmax[i+1] per step and codeword: Max-Log-MAP only (log-MAP forms it from
+                  // the alpha_raw rows on chip; its workspace carries no tmstore region)
     T* llr_out;                 // bare SISO: [G][L][8]
     const int* pi;              // [K] QPP
     const int* pinv;            // [K] inverse QPP
@@ -96,6 +98,7 @@ struct WindowParams {
     int nii;           // boundary metrics from the previous iteration
     int concurrent;    // both SISOs per launch on the previous iteration's extrinsics
     double ext_scale;  // extrinsic scaling (1 = none)
+    int run;           // sub-blocks per lane run, 0 = chosen by window_run (TD_WINDOW_RUN, tests)
 };
 // extra device buffers of the windowed schedule
 template <typename T>
@@ -104,10 +107,15 @@ struct WindowBufs {
     T* ext21[2];
     T* nii;        // [2 parity][2 dec][B][nS][2][8]
     T* ckpt[2];    // per decoder alpha checkpoints (window_ckpt_elems; serial: one shared)
+    uint8_t* bitsT;  // [K][Bp] SISO2's decisions before bits_transpose_kernel (window_bits_bytes)
 };
 // sub-blocks per codeword (the last also takes L mod W) and the checkpoint scratch per decoder
 inline int window_subblocks(int L, int W) { return L / W > 0 ? L / W : 1; }
 size_t window_ckpt_elems(int B, int L, int W, bool f32);
+size_t window_bits_bytes(int B, int K);
+// sub-blocks per lane run of the windowed kernels (1 = one sub-block per lane); `force` > 0 asks for
+// that many where runs are possible (g <= W, W a multiple of the checkpoint spacing S)
+int window_run(int L, int W, int g, int B, int ndec, int S, int force = 0);
 template <typename T>
 hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st);
 

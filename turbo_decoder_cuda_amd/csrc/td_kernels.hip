@@ -15,10 +15,12 @@
 //
 // SISO = Log_MAP_decoder (ITTC/log_map.cpp:898-1047) in the serial schedule of TurboDecoding
 // (:1217-1265).  Per SISO, over windows of kW = 15 trellis steps (12 in the td_kernels_w12.hip build):
-//   F pass  wave A runs alpha forward over the L = K+3 steps and streams alpha of EVERY step (by
-//           state, 512 B per group and step in fp64) and the reference's tempmax (:986-993) to an
-//           HBM scratch (astore / tmstore); Max-Log-MAP stores alpha one step in three and the
-//           folds recompute the steps in between.  No alpha is recomputed in log-MAP.
+//   F pass  wave A runs alpha forward over the L = K+3 steps.  Log-MAP streams the UNNORMALISED
+//           alpha_raw of every step (by state, 512 B per group and step in fp64) and row L to an HBM
+//           scratch (astore [G][L+1][64]); tempmax (:986-993) is the max of such a row, formed on
+//           chip where it is needed.  Max-Log-MAP stores the normalised alpha one step in three and
+//           tempmax (tmstore); its folds recompute the steps in between.  No alpha is recomputed in
+//           log-MAP.
 //   B pass  windows last..first in a three-stage pipeline: wave B runs beta of window t
 //           (subtracting tempmax[i+1], :1019, staged in LDS) and publishes beta by state; the
 //           loader DMAs the alpha rows of window t-1 from the scratch into an LDS ring; the two
@@ -871,8 +873,9 @@ __device__ __forceinline__ StepIn<T> beta_in(const Smem<T>& sm, int tb, int k, i
 // tm_from_alpha; the folds: normalise8), the same exact max and the same subtraction, so the values
 // are bit-identical to streaming alpha[.][i] and tempmax; Max-Log-MAP, which keeps one row in three,
 // streams the normalised checkpoint rows and tempmax[i] (to `ptm`).
-// (A variant that read the max* row of the unnormalised difference ahead of the max, with an
-// exact redo of the window on a bucket mismatch, measured slower: 1098 vs 1203 Mbit/s.)
+// The table row read ahead of the max from the unnormalised difference, with an exact redo of the
+// window on a bucket mismatch, is the kASpec path below (round 1's first form of it measured 1098 vs
+// 1203 Mbit/s; round 4's, with the mismatch flag in a VGPR, +1.3 %: DESIGN.md 3.2).
 template <typename T>
 struct StepHalf {   // a recursion step split at its max* table read (see beta_issue)
     T xs, xp, d, thr, lo, hi;
@@ -2214,7 +2217,7 @@ __global__ __launch_bounds__(kWaves * 64, 2) void siso_kernel(DecodeParams<T> p,
     wg_release(w, p.cu_slots);
 }
 
-// ================================================================== sliding-window mode
+// ================================================================== sub-block schedule
 // BASELINE config 5 / SURVEY.md 8f row 3: the trellis of each codeword is cut into nS sub-blocks
 // of W steps (the last one also takes the remainder, e.g. the 3 tail steps) decoded in parallel.
 // A sub-block's alpha starts g steps early and its beta g steps late (overlap warm-up), from
@@ -2223,28 +2226,36 @@ __global__ __launch_bounds__(kWaves * 64, 2) void siso_kernel(DecodeParams<T> p,
 //     that position in the previous iteration (ITTC/CUDA/turboDecoderBianJieZhi.cu:248,302-304,
 //     312,397-400 -- g = 0 there);
 // only the codeword's first alpha and last beta start from the true initial / terminated states.
-// The SISOs run in the reference's serial order (one launch per SISO) or concurrently (both in one
-// launch, each using the other's extrinsic of the previous iteration: turboDecoderBianJieZhi.cu
-// :642-690), and the extrinsic may be scaled (0.77 there, :423-434).  Each 8-lane group of a wave
-// holds one (decoder, codeword, sub-block) task, so a wave runs 8 independent chains and
-// thousands of waves are in flight: this mode is throughput-bound, not latency-bound.  It is not
-// the reference CPU decoder's arithmetic (window boundaries, butterfly-order LLR fold), so its gate
-// is the BER curve.
+// The SISOs run in the reference's serial order (one launch pair per SISO) or concurrently (both
+// in one launch pair, each using the other's extrinsic of the previous iteration:
+// turboDecoderBianJieZhi.cu:642-690), and the extrinsic may be scaled (0.77 there, :423-434).
+// The arithmetic is oracle/turbo_oracle_window.inc's, which the tests compare with bit for bit:
+// log_map.cpp's steps and left-fold LLR (:975-1039), each chain normalised (:986-1000) only after
+// producing the metric of a position p with (p - sW) a multiple of S (max* is shift-invariant).
 //
-//
-// Layout: one lane per task with the 8 state metrics in registers (the per-state updates are
-// independent: 8-way ILP per lane, no cross-lane traffic), 64 tasks per wave = 64 consecutive
-// codewords of one (decoder, sub-block), so every wave runs the same chain lengths.  The alpha
-// pass keeps only a checkpoint every S steps (HBM scratch, lane-contiguous); the beta pass walks
-// the sub-block in segments of S steps: it loads the segment's inputs once, recomputes the
-// segment's alpha from its checkpoint into registers, then runs beta and the LLR fold backwards
-// over it.  HBM traffic per task-step: the inputs twice plus 8/S alpha values each way.
+// Layout (round 5).  A lane owns one codeword and a RUN of M consecutive sub-blocks [s0, s1) of one
+// decoder; a wave holds 64 consecutive codewords of one run, so every wave walks the same
+// positions and everything but the codeword is wave-uniform.  Two kernels per SISO:
+//   sw_alpha_kernel  alpha forward over the run, a checkpoint every S positions of each sub-block
+//                    to HBM (lane-contiguous).  Over the last g positions of sub-block s the lane
+//                    also runs sub-block s+1's warm-up chain on the same inputs, so the inputs of a
+//                    warm-up are read once for two chains (the round-4 kernel, one sub-block per
+//                    lane, read them twice);
+//   sw_beta_kernel   beta backward over the run in segments of S positions: the segment's alpha
+//                    recomputed from its checkpoint into registers, then beta and the LLR fold;
+//                    over the first g positions of sub-block s, s-1's beta warm-up chain runs beside.
+// Both prefetch the next segment's inputs (and checkpoint) one segment ahead.  SISO2's decisions go
+// to a [K][Bp] byte array (a wave's 64 codewords adjacent) that bits_transpose_kernel turns into
+// [B][K]: written directly, each byte of a wave store landed on its own cache line.
+// Round 4's single kernel (one sub-block per lane, loads waited at each segment start, the
+// interleaver index loaded and waited before every extrinsic store) ran config 5 at 2306-2328 Mbit/s.
 template <typename T>
 struct WinArgs {
     int W, g;              // sub-block length, overlap
     int nS;                // sub-blocks per codeword (the last is L - (nS-1)W long, W..2W-1)
-    int Bp;                // codewords per (decoder, sub-block) rounded up to whole waves
-    int ncp;               // alpha checkpoints per task (ceil(longest sub-block / S))
+    int M, nR;             // sub-blocks per lane run, runs per decoder (nR = ceil(nS / M))
+    int Bp;                // codewords per (decoder, run) rounded up to whole waves
+    int ncp;               // checkpoint slots per sub-block (ceil(longest sub-block / S))
     T ext_scale;
     int dec;               // serial: this launch's SISO; -1: both (concurrent schedule)
     int it;                // iteration
@@ -2254,26 +2265,38 @@ struct WinArgs {
     T* le[2];              // per decoder: Le out, scattered to the other decoder's order
     const T* nii_rd;       // [2 dec][B][nS][2][8]: alpha (0) / beta (1) at the chain's start
     T* nii_wr;
-    T* ckpt[2];            // per decoder: [wave][ncp][8][64] alpha checkpoints
+    T* ckpt[2];            // per decoder: [nS][Bp/64][ncp][8][64] alpha checkpoints
+    uint8_t* bitsT;        // [K][Bp] SISO2's decisions (natural-order rows); null: none this launch
 };
 
 template <typename T>
 struct SwIn {
     T P, Q, ys, la;
 };
+template <typename T>
+struct SwRaw {
+    T ys, yp, la;
+};
 
 // channel + a-priori of (codeword b, step i) of decoder `dec` (steps outside [0, L) clamped)
 template <typename T>
-__device__ __forceinline__ SwIn<T> sw_load(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
+__device__ __forceinline__ SwRaw<T> sw_raw(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
 {
     const int ic = min(max(i, 0), p.L - 1);
     const size_t off = ((size_t)(b >> 3) * p.L + ic) * kCw + (b & 7);
-    const T ys = (dec ? p.sys2 : p.sys1)[off];
-    const T yp = (dec ? p.par2 : p.par1)[off];
-    const T lr = a.la[dec][((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
-    const T la = ic < a.la_len ? lr : (T)0;
+    SwRaw<T> r;
+    r.ys = (dec ? p.sys2 : p.sys1)[off];
+    r.yp = (dec ? p.par2 : p.par1)[off];
+    r.la = a.la[dec][((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
+    return r;
+}
+// the step's P, Q (see "gamma") with La zero where no extrinsic exists (la_ok: i < la_len)
+template <typename T>
+__device__ __forceinline__ SwIn<T> sw_cvt(const SwRaw<T>& r, bool la_ok)
+{
+    const T la = la_ok ? r.la : (T)0;
     const T hla = la / (T)2;
-    return SwIn<T>{(ys + yp) + hla, (ys - yp) + hla, ys, la};
+    return SwIn<T>{(r.ys + r.yp) + hla, (r.ys - r.yp) + hla, r.ys, la};
 }
 
 // gamma of the transition leaving state s with input u: +-(P or Q), see "gamma"
@@ -2283,8 +2306,7 @@ __device__ __forceinline__ T sw_g(const SwIn<T>& x, int s)
     return kTrellisQ[s] ? x.Q : x.P;
 }
 
-// metrics -= their max (log_map.cpp:995-1000).  The windowed chains normalise only every S
-// steps: max* is shift-invariant, and S steps of growth stay far inside the type's range
+// metrics -= their max (log_map.cpp:995-1000), every S positions of the chain's sub-block
 template <typename T>
 __device__ __forceinline__ void sw_normalise(T (&v)[8])
 {
@@ -2293,7 +2315,7 @@ __device__ __forceinline__ void sw_normalise(T (&v)[8])
     for (int j = 0; j < 8; ++j) v[j] = v[j] - m;
 }
 
-// alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-1001)
+// alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-985)
 template <typename T, int ALGO>
 __device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const T* lut)
 {
@@ -2306,8 +2328,25 @@ __device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = n[j];
 }
+// two independent chains on the same step: one code block, so their 16 max* interleave
+template <typename T, int ALGO>
+__device__ __forceinline__ void sw_alpha_step2(T (&a)[8], T (&c)[8], const SwIn<T>& x, const T* lut)
+{
+    T n[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
+        n[j] = mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
+        m[j] = mstar<T, ALGO>(c[p0] - sw_g(x, p0), c[p1] + sw_g(x, p1), lut);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = n[j];
+        c[j] = m[j];
+    }
+}
 
-// beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1021)
+// beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1016)
 template <typename T, int ALGO>
 __device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const T* lut)
 {
@@ -2319,6 +2358,22 @@ __device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const 
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[j] = n[j];
+}
+template <typename T, int ALGO>
+__device__ __forceinline__ void sw_beta_step2(T (&b)[8], T (&c)[8], const SwIn<T>& x, const T* lut)
+{
+    T n[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const T G = sw_g(x, j);
+        n[j] = mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
+        m[j] = mstar<T, ALGO>(c[kTrellisNext[j][0]] - G, c[kTrellisNext[j][1]] + G, lut);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        b[j] = n[j];
+        c[j] = m[j];
+    }
 }
 
 // LLR of step i (log_map.cpp:1024-1039): the two left folds of E over the 8 next states
@@ -2348,137 +2403,349 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
     for (int j = 0; j < 8; ++j) v[j] = (j == 0 || !slot0_only) ? x0 : (T)-kInfty;
 }
 
-// (Four waves per SIMD asked of the register allocator measured 7 % slower in fp64 and +1 % with
-// scratch in fp32: not kept.)
+// the lane's task: decoder, run [s0, s1), codeword b (dead lanes of a partial wave compute on the
+// last codeword and store nothing)
+struct SwTask {
+    int dec, s0, s1, cwv, b;
+    bool live;
+};
+template <typename T>
+__device__ __forceinline__ bool sw_task(const DecodeParams<T>& p, const WinArgs<T>& a, SwTask& t)
+{
+    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const int cw_waves = a.Bp >> 6, per_dec = a.nR * cw_waves;
+    if (wv >= (a.dec < 0 ? 2 : 1) * per_dec) return false;
+    t.dec = a.dec < 0 ? wv / per_dec : a.dec;
+    const int r = wv % per_dec;
+    t.cwv = r % cw_waves;
+    t.s0 = (r / cw_waves) * a.M;
+    t.s1 = min(t.s0 + a.M, a.nS);
+    const int b_raw = t.cwv * 64 + (threadIdx.x & 63);
+    t.live = b_raw < p.B;
+    t.b = t.live ? b_raw : p.B - 1;
+    return true;
+}
+
+template <typename T>
+__device__ __forceinline__ void sw_lut_fill(T* lut_s, const DecodeParams<T>& p)
+{
+    for (int e = threadIdx.x; e < kLutElems<T>; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
+    __syncthreads();
+}
+
+__device__ __forceinline__ int sw_end(int s, int nS, int W, int L) { return s == nS - 1 ? L : (s + 1) * W; }
+__device__ __forceinline__ int floor_div(int x, int m) { return x >= 0 ? x / m : -((-x + m - 1) / m); }
+
+template <typename T>
+__device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s, int c)
+{
+    return a.ckpt[t.dec] + (((size_t)s * (a.Bp >> 6) + t.cwv) * a.ncp + c) * 512 + (threadIdx.x & 63);
+}
+
+// ---- alpha: forward over the run, checkpoints every S positions of each sub-block
 template <typename T, int ALGO, int S>
-__global__ __launch_bounds__(256) void sw_siso_kernel(DecodeParams<T> p, WinArgs<T> a)
+__global__ __launch_bounds__(256) void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[kLutElems<T>];
-    if constexpr (ALGO == 0) {
-        for (int e = threadIdx.x; e < kLutElems<T>; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
-        __syncthreads();
-    }
+    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    SwTask t;
+    if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
     const T* lut = lut_origin(lut_s + (lane % kLutCols<T>));
-    // wave -> (decoder, sub-block, 64 codewords); everything but the codeword is wave-uniform
-    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const int cw_waves = a.Bp >> 6, per_dec = a.nS * cw_waves;
-    if (wv >= (a.dec < 0 ? 2 : 1) * per_dec) return;
-    const int dec = a.dec < 0 ? wv / per_dec : a.dec;
-    const int r = wv % per_dec;            // wave within the decoder: checkpoint block
-    const int s = r / cw_waves;
-    const int b_raw = (r % cw_waves) * 64 + lane;
-    const bool live = b_raw < p.B;
-    const int b = live ? b_raw : p.B - 1;
-    const int i0 = s * a.W - a.g;
-    const int len = s == a.nS - 1 ? p.L - s * a.W : a.W;
-    const size_t nii = (((size_t)dec * p.B + b) * a.nS + s) * 16;
-    T* ck = a.ckpt[dec] + (size_t)r * a.ncp * 8 * 64 + lane;
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, dec = t.dec, b = t.b;
+    T* const niw = a.nii_wr + ((size_t)dec * p.B + b) * nS * 16;
+    const T* const nir = a.nii_rd + ((size_t)dec * p.B + b) * nS * 16;
+    const bool use_nii = a.nii && a.it > 0;
+    const int base0 = t.s0 * W;
 
-    // ---- alpha: from relative index 0 (absolute i0; steps before 0 are skipped) to g + len,
-    // a checkpoint at every S-th step of the sub-block, the NII alpha of sub-block s+1 at W
-    T al[8];
+    // the chain of sub-block s0 starts at i0 (clamped to 0)
+    T al[8], bl[8];
+    const int i0 = base0 - g;
     if (i0 <= 0)
         sw_set(al, 1, (T)0);
-    else if (a.nii && a.it > 0)
+    else if (use_nii)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) al[j] = a.nii_rd[nii + j];
+        for (int j = 0; j < 8; ++j) al[j] = nir[(size_t)t.s0 * 16 + j];
     else
         sw_set(al, 0, (T)0);
-    const int n = a.g + len;
-    for (int k0 = max(0, -i0); k0 <= n; k0 += S) {
-        SwIn<T> x[S];
+    sw_set(bl, 0, (T)0);
+    const int ps = max(i0, 0);
+
+    // per sub-block bookkeeping (wave-uniform)
+    int s = t.s0, st = 0, en = 0, qb = 0, need = 0;
+    bool hasB = false;
+    auto enter = [&](int ns) {
+        s = ns;
+        st = s * W;
+        en = sw_end(s, nS, W, L);
+        hasB = s + 1 < t.s1;                     // the next sub-block's chain runs in this lane
+        qb = st + W - g;                         // its start = the NII alpha position of s+1
+        const int lc = st + ((en - st - 1) / S) * S;   // last checkpoint
+        need = s < nS - 1 ? max(lc, qb) : lc;    // alpha wanted up to here
+    };
+    enter(t.s0);
+    if (s < nS - 1 && qb < 0 && t.live)          // (g > W) the NII position lies before step 0
 #pragma unroll
-        for (int m = 0; m < S; ++m) x[m] = sw_load(p, a, dec, b, i0 + k0 + m);
+        for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = j == 0 ? (T)0 : (T)-kInfty;
+    const int stop = [&] {                        // the run's last position with work
+        const int sl = t.s1 - 1, stl = sl * W, enl = sw_end(sl, nS, W, L);
+        const int lc = stl + ((enl - stl - 1) / S) * S;
+        return sl < nS - 1 ? max(lc, stl + W - g) : lc;
+    }();
+
+    int bp = base0 + floor_div(ps - base0, S) * S;
+    SwRaw<T> nx[S];
+#pragma unroll
+    for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, bp + m);
+    for (; bp <= stop; bp += S) {
+        SwRaw<T> cx[S];
 #pragma unroll
         for (int m = 0; m < S; ++m) {
-            const int k = k0 + m;
-            if (k > n) break;
-            if (k >= a.g && k < n && ((k - a.g) % S) == 0) {
-                sw_normalise(al);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ck[((size_t)((k - a.g) / S) * 8 + j) * 64] = al[j];
-            } else if (k < a.g && m == 0) {
-                sw_normalise(al);   // warm-up
-            }
-            if (k == a.W && s < a.nS - 1 && live)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) a.nii_wr[nii + 16 + j] = al[j];
-            if (k < n) sw_alpha_step<T, ALGO>(al, x[m], lut);
-        }
-    }
-    if (-i0 > a.W && s < a.nS - 1 && live)   // the NII position lies before step 0: the initial state
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a.nii_wr[nii + 16 + j] = j == 0 ? (T)0 : (T)-kInfty;
-
-    // ---- beta: warm-up from relative index len + 2g (absolute end + g) down to g + len
-    T be[8];
-    const int top = len + 2 * a.g;   // beta[.][i0 + top] starts the chain
-    if (i0 + top >= p.L)
-        sw_set(be, 1, (T)0);
-    else if (a.nii && a.it > 0)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) be[j] = a.nii_rd[nii + 8 + j];
-    else
-        sw_set(be, 0, (T)0);
-    auto nii_beta = [&](int kr) {   // beta[.][i0 + kr] is the NII beta of sub-block s-1 at kr = 2g
-        if (kr == 2 * a.g && s > 0 && live)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) a.nii_wr[nii - 16 + 8 + j] = be[j];
-    };
-    if (2 * a.g >= p.L - i0) nii_beta(2 * a.g);   // NII position at or past L: the terminated state
-    for (int kr = min(top, p.L - i0) - 1; kr >= n; --kr) {   // beyond L the terminated state holds
-        sw_beta_step<T, ALGO>(be, sw_load(p, a, dec, b, i0 + kr), lut);
-        if (kr % S == 0) sw_normalise(be);
-        nii_beta(kr);
-    }
-
-    // ---- the sub-block, segment by segment from the last: inputs, alpha from the checkpoint,
-    // then beta + LLR backwards
-    const bool want_bits = dec == 1 && (p.all_iters || a.it == p.iters - 1);
-    for (int c = (len - 1) / S; c >= 0; --c) {
-        const int kb = a.g + c * S;   // relative index of the segment's first step
-        SwIn<T> x[S];
-        T as[S][8];
-#pragma unroll
-        for (int m = 0; m < S; ++m) x[m] = sw_load(p, a, dec, b, i0 + kb + m);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) as[0][j] = ck[((size_t)c * 8 + j) * 64];
-#pragma unroll
-        for (int m = 1; m < S; ++m) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) as[m][j] = as[m - 1][j];
-            if (kb + m < n) sw_alpha_step<T, ALGO>(as[m], x[m - 1], lut);
+            cx[m] = nx[m];
+            nx[m] = sw_raw(p, a, dec, b, bp + S + m);   // next segment, one segment ahead
         }
 #pragma unroll
-        for (int m = S - 1; m >= 0; --m) {
-            const int kr = kb + m, i = i0 + kr;
-            if (kr >= n) continue;
-            const T llr = sw_llr<T, ALGO>(as[m], be, x[m], lut);
-            if (live) {
-                const T le = (llr - x[m].la - (T)2 * x[m].ys) * a.ext_scale;
-                if (i < p.K) {
-                    const int w = dec ? p.pi[i] : p.pinv[i];
-                    a.le[dec][((size_t)(b >> 3) * p.K + w) * kCw + (b & 7)] = le;
-                    if (want_bits)
-                        p.bits[(size_t)b * (p.all_iters ? p.iters * p.K : p.K) + (size_t)(p.all_iters ? a.it : 0) * p.K +
-                               p.pi[i]] = llr < (T)0 ? 0 : 1;
-                }
-                if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * p.L + (size_t)(2 * a.it + dec) * p.L + i] = le;
+        for (int m = 0; m < S; ++m) {
+            const int pos = bp + m;
+            if (pos < ps || pos > stop) continue;
+            if (m == 0 && pos >= st && pos < en) {       // checkpoint alpha[pos] (normalised)
+                T* ck = sw_ck(a, t, s, (pos - st) / S);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ck[j * 64] = al[j];
             }
-            sw_beta_step<T, ALGO>(be, x[m], lut);
-            if (m == 0) sw_normalise(be);
-            nii_beta(kr);
+            if (s < nS - 1 && pos == qb && t.live)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
+            if (hasB && pos == qb) {                     // sub-block s+1's chain starts here
+                if (qb <= 0)
+                    sw_set(bl, 1, (T)0);
+                else if (use_nii)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
+                else
+                    sw_set(bl, 0, (T)0);
+            }
+            const SwIn<T> x = sw_cvt(cx[m], pos < a.la_len);
+            const bool doA = pos < need, doB = hasB && pos >= qb;
+            if (doA && doB)
+                sw_alpha_step2<T, ALGO>(al, bl, x, lut);
+            else if (doA)
+                sw_alpha_step<T, ALGO>(al, x, lut);
+            else if (doB)
+                sw_alpha_step<T, ALGO>(bl, x, lut);
+            if (m == S - 1) {                            // alpha[bp + S]: an aligned position
+                if (doA) sw_normalise(al);
+                if (doB) sw_normalise(bl);
+            }
+        }
+        if (hasB && bp + S == en) {                      // hand over to sub-block s+1
+            if (qb >= en) {                              // g = 0: its chain starts at its first position
+                if (t.live)                              // (alpha[en] of this chain is its NII metric)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
+                if (use_nii)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
+                else
+                    sw_set(bl, 0, (T)0);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) al[j] = bl[j];
+            enter(s + 1);
         }
     }
 }
 
-// checkpoint spacing S: the segment's alpha stays in registers.  fp64: 4 (2 -- 4 waves/SIMD, half the
-// recompute, twice the checkpoint traffic -- measured -12 %; 3 and 5 -6 %); fp32: 8.
+// ---- beta + LLR: backward over the run in segments of S positions
+template <typename T, int ALGO, int S>
+__global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
+                                                      const int* __restrict__ pinv)
+{
+    __shared__ T lut_s[kLutElems<T>];
+    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    SwTask t;
+    if (!sw_task(p, a, t)) return;
+    const int lane = threadIdx.x & 63;
+    const T* lut = lut_origin(lut_s + (lane % kLutCols<T>));
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, b = t.b;
+    T* const niw = a.nii_wr + ((size_t)dec * p.B + b) * nS * 16;
+    const T* const nir = a.nii_rd + ((size_t)dec * p.B + b) * nS * 16;
+    const bool use_nii = a.nii && a.it > 0;
+    const int base0 = t.s0 * W;
+    const int* const perm = dec ? pi : pinv;
+    T* const le = a.le[dec] + (size_t)(b >> 3) * K * kCw + (b & 7);
+    uint8_t* const bitsT = dec ? a.bitsT : nullptr;
+    const int bcol = t.cwv * 64 + lane;
+
+    int s = t.s1 - 1, st = 0, en = 0, qb = 0;
+    bool hasB = false;
+    auto enter = [&](int ns) {
+        s = ns;
+        st = s * W;
+        en = sw_end(s, nS, W, L);
+        hasB = s > t.s0;                          // the previous sub-block's chain runs in this lane
+        qb = min(st + g, L);                      // its start (= the NII beta position of s-1)
+    };
+    enter(t.s1 - 1);
+    // the chain of sub-block s1-1 starts at e = end + g (clamped to L)
+    T be[8], bb[8];
+    const int e = en + g;
+    if (e >= L)
+        sw_set(be, 1, (T)0);
+    else if (use_nii)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) be[j] = nir[(size_t)s * 16 + 8 + j];
+    else
+        sw_set(be, 0, (T)0);
+    sw_set(bb, 0, (T)0);
+    if (s > 0 && st + g >= L && t.live)           // NII position at or past L: the terminated state
+#pragma unroll
+        for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = j == 0 ? (T)0 : (T)-kInfty;
+    const int pe = min(e, L) - 1;                 // first position stepped
+
+    // segment prefetch: inputs and, for a segment of a sub-block's own range, its checkpoint
+    auto seg_sub = [&](int sbp) {                 // sub-block whose chain covers segment sbp
+        return sbp >= en ? s : min(t.s0 + (sbp - base0) / W, t.s1 - 1);
+    };
+    int bp = base0 + floor_div(pe - base0, S) * S;
+    SwRaw<T> nx[S];
+    T nck[8] = {};
+    auto prefetch = [&](int nbp) {
+#pragma unroll
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, nbp + m);
+        const int ns = seg_sub(nbp), nst = ns * W;
+        if (nbp >= base0 && nbp < sw_end(ns, nS, W, L)) {
+            const T* ck = sw_ck(a, t, ns, (nbp - nst) / S);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nck[j] = ck[j * 64];
+        }
+    };
+    prefetch(bp);
+    for (; bp >= base0; bp -= S) {
+        SwRaw<T> cx[S];
+        T as[S][8];
+#pragma unroll
+        for (int m = 0; m < S; ++m) cx[m] = nx[m];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) as[0][j] = nck[j];
+        if (bp - S >= base0) prefetch(bp - S);
+        SwIn<T> x[S];
+#pragma unroll
+        for (int m = 0; m < S; ++m) x[m] = sw_cvt(cx[m], bp + m < a.la_len);
+        const bool main = bp < en;                        // the segment lies in sub-block s's own range
+        if (main) {                                       // alpha of the segment from its checkpoint
+#pragma unroll
+            for (int m = 1; m < S; ++m) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) as[m][j] = as[m - 1][j];
+                if (bp + m < en) sw_alpha_step<T, ALGO>(as[m], x[m - 1], lut);
+            }
+        }
+#pragma unroll
+        for (int m = S - 1; m >= 0; --m) {
+            const int pos = bp + m;
+            if (pos > pe) continue;
+            if (main && pos < en) {                       // LLR, extrinsic, decision (beta = beta[pos + 1])
+                const T llr = sw_llr<T, ALGO>(as[m], be, x[m], lut);
+                const T lev = (llr - x[m].la - (T)2 * x[m].ys) * a.ext_scale;
+                if (t.live) {
+                    if (pos < K) {
+                        le[(size_t)perm[pos] * kCw] = lev;
+                        if (bitsT) bitsT[(size_t)pi[pos] * a.Bp + bcol] = llr < (T)0 ? 0 : 1;
+                    }
+                    if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
+                }
+            }
+            if (hasB && pos == qb - 1) {                  // sub-block s-1's chain starts at qb
+                if (qb >= L)
+                    sw_set(bb, 1, (T)0);
+                else if (use_nii)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
+                else
+                    sw_set(bb, 0, (T)0);
+            }
+            const bool doB = hasB && pos < qb;
+            if (doB)
+                sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
+            else
+                sw_beta_step<T, ALGO>(be, x[m], lut);
+            if (m == 0) {                                 // beta[bp]: an aligned position
+                sw_normalise(be);
+                if (doB) sw_normalise(bb);
+            }
+            if (s > 0 && pos == st + g && t.live)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
+        }
+        if (hasB && bp == st) {                           // hand over to sub-block s-1
+            if (qb <= st) {                               // g = 0: its chain starts at its end
+                if (use_nii)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
+                else
+                    sw_set(bb, 0, (T)0);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) be[j] = bb[j];
+            enter(s - 1);
+            if (s > 0 && st + g == en && t.live)          // g = W: the NII position is this chain's start
+#pragma unroll
+                for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
+        }
+    }
+}
+
+// SISO2's decisions [K][Bp] (rows in natural order) -> bits [B][K] (row stride `stride`): 64 x 64-byte
+// tiles through LDS, 16-byte loads and stores
+__global__ __launch_bounds__(256) void bits_transpose_kernel(const uint8_t* __restrict__ src, int K, int Bp, int B,
+                                                             uint8_t* __restrict__ dst, long long stride)
+{
+    __shared__ uint8_t tile[64][64 + 16];
+    const int k0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    const int r = threadIdx.x >> 2, q = (threadIdx.x & 3) * 16;
+    if (k0 + r < K) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)(k0 + r) * Bp + b0 + q);
+        *reinterpret_cast<uint4*>(&tile[r][q]) = v;
+    }
+    __syncthreads();
+    const int b = b0 + r;
+    if (b >= B) return;
+    uint8_t o[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) o[u] = tile[q + u][r];
+    uint8_t* d = dst + (size_t)b * stride + k0 + q;
+    if (k0 + q + 16 <= K && ((reinterpret_cast<size_t>(d) & 15) == 0)) {
+        *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(o);
+    } else {
+        for (int u = 0; u < 16 && k0 + q + u < K; ++u) d[u] = o[u];
+    }
+}
+
+// checkpoint spacing S: the segment's alpha stays in registers.  fp64: 4 (round 4: 2 measured -12 %,
+// 3 and 5 -6 %); fp32: 8.
 template <typename T>
 constexpr int sw_seg()
 {
     return sizeof(T) == 4 ? 8 : 4;
+}
+
+// sub-blocks per lane run: one (M = 1) while a launch has fewer than kSwRunWaves one-sub-block waves,
+// else as many as keep about that many waves; runs need g <= W (two chains at most) and W a multiple
+// of S (every sub-block start is a segment start)
+#ifndef TD_SW_RUN_WAVES
+#define TD_SW_RUN_WAVES 8192
+#endif
+constexpr int kSwRunWaves = TD_SW_RUN_WAVES;
+
+int window_run(int L, int W, int g, int B, int ndec, int S, int force)
+{
+    const int nS = window_subblocks(L, W);
+    if (g > W || W % S != 0) return 1;
+    if (force > 0) return force < nS ? force : nS;
+    const long long waves = (long long)nS * ((B + 63) / 64) * ndec;
+    const long long m = waves / kSwRunWaves;
+    return m < 1 ? 1 : (m > nS ? nS : (int)m);
 }
 
 template <typename T, int ALGO>
@@ -2487,10 +2754,13 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     constexpr int S = sw_seg<T>();
     const int W = w.window;
     const int nS = window_subblocks(p.L, W);
+    const int ndec = w.concurrent ? 2 : 1;
     WinArgs<T> a{};
     a.W = W;
     a.g = w.overlap;
     a.nS = nS;
+    a.M = window_run(p.L, W, w.overlap, p.B, ndec, S, w.run);
+    a.nR = (nS + a.M - 1) / a.M;
     a.Bp = (p.B + 63) / 64 * 64;
     a.ncp = (p.L - (nS - 1) * W + S - 1) / S;
     a.ext_scale = (T)w.ext_scale;
@@ -2498,10 +2768,14 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.ckpt[0] = wb.ckpt[0];
     a.ckpt[1] = wb.ckpt[1];
     const size_t nii_half = (size_t)2 * p.B * nS * 16;
+    const long long waves = (long long)a.nR * (a.Bp / 64) * ndec;
+    const int blocks = (int)((waves + 3) / 4);
     for (int it = 0; it < p.iters; ++it) {
         a.it = it;
         a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
         a.nii_wr = wb.nii + (size_t)(it & 1) * nii_half;
+        const bool want_bits = p.all_iters || it == p.iters - 1;
+        a.bitsT = want_bits ? wb.bitsT : nullptr;
         for (int dec = 0; dec < (w.concurrent ? 1 : 2); ++dec) {
             if (w.concurrent) {   // Jacobi: both SISOs read the other's Le of iteration it-1
                 a.dec = -1;
@@ -2516,9 +2790,15 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 a.la[0] = a.le[1] = wb.ext21[0];
                 a.la[1] = a.le[0] = wb.ext12[0];
             }
-            const long long waves = (long long)nS * (a.Bp / 64) * (w.concurrent ? 2 : 1);
-            const int blocks = (int)((waves + 3) / 4);
-            hipLaunchKernelGGL((sw_siso_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a);
+            hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a);
+            hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a, p.pi, p.pinv);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        if (want_bits) {
+            const long long stride = p.all_iters ? (long long)p.iters * p.K : p.K;
+            hipLaunchKernelGGL(bits_transpose_kernel, dim3((p.K + 63) / 64, a.Bp / 64), dim3(256), 0, st, wb.bitsT,
+                               p.K, a.Bp, p.B, p.bits + (p.all_iters ? (size_t)it * p.K : 0), stride);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -2533,6 +2813,8 @@ size_t window_ckpt_elems(int B, int L, int W, bool f32)
     const size_t ncp = (size_t)(L - (nS - 1) * W + S - 1) / S;
     return (size_t)nS * ((B + 63) / 64) * ncp * 8 * 64;
 }
+
+size_t window_bits_bytes(int B, int K) { return (size_t)K * ((B + 63) / 64) * 64; }
 
 template <typename T>
 hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)

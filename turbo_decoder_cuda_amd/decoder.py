@@ -77,6 +77,14 @@ class TurboCodec:
         n = N.lib().td_debug_placement(self._h, ms, n, C.byref(pick))
         return [round(ms[i], 4) for i in range(n)], pick.value
 
+    def placement_cost(self):
+        """(wall ms, peak bytes of candidate workspaces held) of that search (td_debug_placement_cost)."""
+        if not hasattr(N.lib(), "td_debug_placement_cost"):
+            return None, None
+        w, b = C.c_double(0), C.c_double(0)
+        N.check(N.lib().td_debug_placement_cost(self._h, C.byref(w), C.byref(b)))
+        return w.value, b.value
+
     def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
                    concurrent: bool = False) -> None:
         """Windowed schedule (td_set_window; BASELINE config 5); window=0: exact.
