@@ -124,6 +124,46 @@ def load_traffic(cfg_key):
         return None
 
 
+def load_traffic_rec(cfg_key):
+    """The whole profiles/traffic.json record of a configuration (None if absent)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "traffic.json")) as f:
+            return json.load(f).get(cfg_key)
+    except (OSError, ValueError):
+        return None
+
+
+N_SIMDS = 1024   # 256 CUs x 4 SIMDs (MI355X)
+
+
+def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
+    """Roofline record of the windowed schedule (BASELINE config 5: fp64 log-MAP, window 64, overlap 30)
+    from the live decode time and the committed PMC of the same kernels (profiles/traffic.json key
+    K6144_B32768_it8_f64_logmap_w64g30: FETCH_SIZE x2 + WRITE_SIZE bytes and SQ_INSTS_VALU per decode,
+    scripts/gpu_r5_wpmc.sh).  Two bounds: VALU issue (a wave64 fp64 VALU instruction occupies its SIMD
+    4 cycles; 1024 SIMDs at the shader clock) and HBM (counter bytes against the 8 TB/s spec and the
+    6.29 TB/s streaming ceiling).  The algorithmic-bytes fraction is the metric's contract, as for
+    the exact kernel."""
+    rec = load_traffic_rec(f"K{K}_B{B}_it{iters}_f64_logmap_w64g30")
+    clk = sclk_ghz or SCLK_GHZ
+    alg = B * (8 * (3 * K + 12) + K)
+    out = {"kernels": "sw_demux_kernel + (sw_alpha_kernel + sw_beta_kernel) x 2 SISOs x iterations + bits_transpose",
+           "decode_ms": round(decode_ms, 4), "alg_bytes_per_decode": alg,
+           "achieved": round(alg / (decode_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg / (decode_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)}
+    if rec:
+        tb = float(rec["bytes_per_decode"])
+        vi = float(rec["valu_instr_per_decode"])
+        cap = N_SIMDS * clk * 1e9 / 4.0 * decode_ms * 1e-3   # wave-instructions the SIMDs could issue
+        out.update({"traffic": int(tb), "traffic_gbs": round(tb / (decode_ms * 1e-3) / 1e9, 1),
+                    "traffic_frac": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_frac_measured_ceiling": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_MEASURED_GBS, 4),
+                    "valu_instr_per_decode": int(vi), "valu_issue_frac": round(vi / cap, 4),
+                    "sclk_ghz": round(clk, 4), "sclk_source": "power record (amdsmi)" if sclk_ghz else "constant",
+                    "pmc_source": rec.get("source"), "kernel": rec.get("kernel")})
+    return out
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -550,7 +590,7 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "sw_siso_kernel" if a.window else "turbo_decode_kernel",
+            "kernel": "sw_alpha_kernel + sw_beta_kernel" if a.window else "turbo_decode_kernel",
             "achieved": round(achieved, 3),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -566,13 +606,15 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2,
             "clock_span_ms": round(clock[1], 4) if clock else None,
             "limiter": ("latency of the serial alpha / beta recursions (one dependent trellis step at a time "
                         "per codeword; DESIGN.md 3.2): neither HBM nor VALU is saturated") if not a.window else
-                       "VALU / LDS issue of the sub-block chains (DESIGN.md 8.3)",
+                       "VALU issue and HBM of the sub-block kernels together (DESIGN.md 8.3; `window`)",
             "valu_top_s": round(valu_tops, 3),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_codeword": bytes_cw,
             "kernel_ms_avg": round(turbo_ms, 4),
             "demux_ms_avg": round(demux_ms, 4),
             "launches_timed": nlaunch,
+            "window": (window_roofline(a.K, a.batch, a.iters, demux_ms + turbo_ms)
+                       if a.window and a.precision == "f64" and a.algo == "logmap" and turbo_ms > 0 else None),
         },
         "ber": {"bit_errors": errs, "block_errors": blk,
                 "ber": errs / (world * a.batch * a.K), "bler": blk / (world * a.batch)},
@@ -761,6 +803,8 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
                                else ("3" if algo == "maxlog" and prec == "f64" else None))
         res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B, "config": cfg,
                     "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
+        if win and prec == "f64" and algo == "logmap":
+            res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3)
     if big is not None and a.K == 6144:
         res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
     return res

@@ -96,6 +96,7 @@ struct td_handle {
     td::WindowParams wp{0, 0, 0, 0, 1.0, 0};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
+    td::WindowStreams wstr{nullptr, nullptr, nullptr};   // the windowed schedule's second stream (halves)
     // Workspace ordering across streams: every decode uses the same d_ws / d_wws, so a decode
     // issued on a stream other than the previous decode's first waits (on the device) for that
     // decode to finish with the workspace.  Decodes on one handle therefore never overlap; callers
@@ -179,8 +180,10 @@ struct Carve {
 Carve carve(int G, int K, size_t elem, int algo, bool exact)
 {
     const int L = K + td::kMemory;
-    const size_t arrL = align_up((size_t)G * L * 8 * elem, 256);
-    const size_t arrK = align_up((size_t)G * K * 8 * elem, 256);
+    // codewords: groups of 8 (exact schedule) or the windowed schedule's wide groups of 64
+    const size_t ncw = exact ? (size_t)G * 8 : ((size_t)G * 8 + 63) / 64 * 64;
+    const size_t arrL = align_up(ncw * L * elem, 256);
+    const size_t arrK = align_up(ncw * K * elem, 256);
     const size_t arrA = exact ? align_up(td::astore_elems(G, L) * elem, 256) : 0;
     const size_t arrT = exact && algo == TD_ALGO_MAXLOG ? arrL : 0;
     Carve c{};
@@ -389,7 +392,7 @@ WinCarve win_carve(const td_handle* h, int B)
     const size_t elem = h->elem;
     const int K = h->p.K, L = K + td::kMemory, G = groups_for(B);
     WinCarve c{};
-    c.arrK = align_up((size_t)G * K * 8 * elem, 256);
+    c.arrK = align_up(((size_t)B + 63) / 64 * 64 * K * elem, 256);   // wide groups of 64 codewords
     c.nii = (size_t)2 * 2 * B * td::window_subblocks(L, h->wp.window) * 16 * elem;
     c.arrC = align_up(td::window_ckpt_elems(B, L, h->wp.window, elem == 4) * elem, 256);
     c.nii = align_up(c.nii, 256);
@@ -497,11 +500,18 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
         ev = h->ev[h->nev].data();   // claimed (nev advanced) only once all three are recorded
         TD_HIP(hipEventRecord(ev[0], st));
     }
-    hipError_t e = td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
+    hipError_t e = h->wp.window ? td::launch_window_demux<T>(dp, static_cast<const T*>(d_llr), st)
+                                : td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
-    if (h->wp.window)
-        e = td::launch_window<T>(dp, h->wp, wb, st);
+    if (h->wp.window) {
+        if (!h->wstr.st2) {   // created once, on the handle's device (the decode's caller stream is the first)
+            TD_HIP(hipStreamCreateWithFlags(&h->wstr.st2, hipStreamNonBlocking));
+            TD_HIP(hipEventCreateWithFlags(&h->wstr.fork, hipEventDisableTiming));
+            TD_HIP(hipEventCreateWithFlags(&h->wstr.join, hipEventDisableTiming));
+        }
+        e = td::launch_window<T>(dp, h->wp, wb, st, h->wstr);
+    }
     else
         e = td::launch_turbo<T>(dp, st);
     if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
@@ -788,6 +798,9 @@ int td_destroy(td_handle* h)
     if (h->d_hle) (void)hipFree(h->d_hle);
     if (h->d_win) (void)hipFree(h->d_win);
     if (h->d_wws) (void)hipFree(h->d_wws);
+    if (h->wstr.st2) (void)hipStreamDestroy(h->wstr.st2);
+    if (h->wstr.fork) (void)hipEventDestroy(h->wstr.fork);
+    if (h->wstr.join) (void)hipEventDestroy(h->wstr.join);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     if (h->ws_free) (void)hipEventDestroy(h->ws_free);

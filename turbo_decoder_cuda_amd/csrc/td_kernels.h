@@ -83,6 +83,9 @@ struct DecodeParams {
 // demultiplex + x0.5 of the stream into the batch-interleaved arrays
 template <typename T>
 hipError_t launch_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st);
+// the same into the windowed schedule's wide arrays [B/64][L][64] (sys2 included)
+template <typename T>
+hipError_t launch_window_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st);
 // the turbo iterations (one wave per 8 codewords)
 template <typename T>
 hipError_t launch_turbo(const DecodeParams<T>& p, hipStream_t st, bool probe = false);   // probe: td_reserve's placement probe symbol
@@ -103,7 +106,7 @@ struct WindowParams {
 // extra device buffers of the windowed schedule
 template <typename T>
 struct WindowBufs {
-    T* ext12[2];   // [G][K][8] x2 (concurrent schedule: iteration parity); serial uses [0]
+    T* ext12[2];   // [B/64][K][64] x2 (concurrent schedule: iteration parity); serial uses [0]
     T* ext21[2];
     T* nii;        // [2 parity][2 dec][B][nS][2][8]
     T* ckpt[2];    // per decoder alpha checkpoints (window_ckpt_elems; serial: one shared)
@@ -116,8 +119,14 @@ size_t window_bits_bytes(int B, int K);
 // sub-blocks per lane run of the windowed kernels (1 = one sub-block per lane); `force` > 0 asks for
 // that many where runs are possible (g <= W, W a multiple of the checkpoint spacing S)
 int window_run(int L, int W, int g, int B, int ndec, int S, int force = 0);
+// the handle's second stream and its fork / join events (timing disabled); st2 null: one stream
+struct WindowStreams {
+    hipStream_t st2;
+    hipEvent_t fork, join;
+};
 template <typename T>
-hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st);
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st,
+                         const WindowStreams& ws);
 
 template <typename T>
 hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* la_ws, int terminated, T* llr,

@@ -70,6 +70,7 @@ constexpr unsigned kDiagNoAdma = 1;       // the B pass without the loader's alp
 constexpr unsigned kDiagNoBConvert = 2;   // the B pass without the loader's tile / tempmax converts
 constexpr unsigned kDiagNoFold = 4;       // the B pass without its folds
 constexpr unsigned kDiagNoBeta = 8;       // the B pass without the beta chain
+constexpr unsigned kDiagOcc3Alias = 16;   // beta rows and tile ring alias the alpha ring: fp64 three per CU (Smem)
 template <unsigned D>
 constexpr bool kDiag = (TD_DIAG & D) != 0;
 
@@ -389,10 +390,25 @@ static_assert(kStageBytes<double> % 16 == 0 && kStageBytes<float> % 16 == 0, "16
 template <typename T>
 struct Smem {
     T lut[kLutElems<T>];   // max* table: [bucket][thr | v][kLutCols columns] (see lut_origin)
+#if (TD_DIAG & 16) != 0
+    // timing-only build (kDiagOcc3Alias, results WRONG): the beta rows and the tile ring alias the
+    // alpha ring, so an fp64 workgroup fits three per CU (52.7 KB) with every DMA, store and
+    // instruction of the product kept -- the upper bound of a three-per-CU fp64 kernel.
+    // The write positions (Wp) and the staging slots stay apart, so every global store stays in range.
+    union {
+        alignas(16) T Av[kAvSlots][kW][kLanes];
+        struct {
+            alignas(16) T Bv[2][kW][kLanes];
+            T G[3][kW][kCw][4];
+        };
+    };
+    alignas(8) int Wp[3][kW][2];
+#else
     T G[3][kW][kCw][4];        // (P, Q, ys, La) per step and codeword, ring by window index mod 3
     alignas(8) int Wp[3][kW][2];   // extrinsic / decision write positions (pi or pinv, pi) per step, same ring
     alignas(16) T Av[kAvSlots][kW][kLanes];   // [window mod 4] alpha[.][i] by 8c + state (fold input, DMA from HBM)
     alignas(16) T Bv[2][kW][kLanes];       // [window parity] beta[.][i+1] by 8c + state (fold input)
+#endif
     alignas(16) T tm[2][kW][kCw];          // [window parity] tempmax[i+1] per step and codeword (beta input)
     // loader: staged window inputs, slots 0-2 (window t in slot t % 3); Max-Log-MAP keeps its three
     // staged tempmax windows in slot 3
@@ -2254,7 +2270,8 @@ struct WinArgs {
     int W, g;              // sub-block length, overlap
     int nS;                // sub-blocks per codeword (the last is L - (nS-1)W long, W..2W-1)
     int M, nR;             // sub-blocks per lane run, runs per decoder (nR = ceil(nS / M))
-    int Bp;                // codewords per (decoder, run) rounded up to whole waves
+    int Bp;                // the batch's codewords rounded up to whole waves (row stride of bitsT / ckpt)
+    int cw0, ncw;          // this launch's slice of the batch: waves of 64 codewords [cw0, cw0 + ncw)
     int ncp;               // checkpoint slots per sub-block (ceil(longest sub-block / S))
     T ext_scale;
     int dec;               // serial: this launch's SISO; -1: both (concurrent schedule)
@@ -2278,16 +2295,22 @@ struct SwRaw {
     T ys, yp, la;
 };
 
+// The windowed schedule's arrays are WIDE (round 5): [B/64][L][64] and [B/64][K][64], the 64 codewords
+// of a wave adjacent per step, so a wave's load of one step is one 512-byte row (4 whole cache lines)
+// and its extrinsic store one 512-byte row at the interleaved position.  (The exact schedule keeps its
+// 8-codeword groups; sw_demux_kernel writes this layout.)  Round 4 read the 8-codeword layout: eight
+// 64-byte pieces per wave load, half a cache line each.
+constexpr int kSwCw = 64;
 // channel + a-priori of (codeword b, step i) of decoder `dec` (steps outside [0, L) clamped)
 template <typename T>
 __device__ __forceinline__ SwRaw<T> sw_raw(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
 {
     const int ic = min(max(i, 0), p.L - 1);
-    const size_t off = ((size_t)(b >> 3) * p.L + ic) * kCw + (b & 7);
+    const size_t off = ((size_t)(b >> 6) * p.L + ic) * kSwCw + (b & 63);
     SwRaw<T> r;
     r.ys = (dec ? p.sys2 : p.sys1)[off];
     r.yp = (dec ? p.par2 : p.par1)[off];
-    r.la = a.la[dec][((size_t)(b >> 3) * p.K + min(ic, p.K - 1)) * kCw + (b & 7)];
+    r.la = a.la[dec][((size_t)(b >> 6) * p.K + min(ic, p.K - 1)) * kSwCw + (b & 63)];
     return r;
 }
 // the step's P, Q (see "gamma") with La zero where no extrinsic exists (la_ok: i < la_len)
@@ -2376,6 +2399,17 @@ __device__ __forceinline__ void sw_beta_step2(T (&b)[8], T (&c)[8], const SwIn<T
     }
 }
 
+// A scheduling fence between the positions of a fast segment: without it the scheduler hoists the
+// next position's table reads into the current one and the beta kernel needs 298 VGPRs (one wave per
+// SIMD); with it a position's live set is the per-position path's.
+#ifndef TD_SW_FENCE
+#define TD_SW_FENCE 1
+#endif
+__device__ __forceinline__ void sw_fence()
+{
+    if constexpr (TD_SW_FENCE) __builtin_amdgcn_sched_barrier(0);
+}
+
 // LLR of step i (log_map.cpp:1024-1039): the two left folds of E over the 8 next states
 template <typename T, int ALGO>
 __device__ __forceinline__ T sw_llr(const T (&a)[8], const T (&b)[8], const SwIn<T>& x, const T* lut)
@@ -2413,11 +2447,11 @@ template <typename T>
 __device__ __forceinline__ bool sw_task(const DecodeParams<T>& p, const WinArgs<T>& a, SwTask& t)
 {
     const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const int cw_waves = a.Bp >> 6, per_dec = a.nR * cw_waves;
+    const int cw_waves = a.ncw, per_dec = a.nR * cw_waves;
     if (wv >= (a.dec < 0 ? 2 : 1) * per_dec) return false;
     t.dec = a.dec < 0 ? wv / per_dec : a.dec;
     const int r = wv % per_dec;
-    t.cwv = r % cw_waves;
+    t.cwv = a.cw0 + r % cw_waves;   // absolute wave of 64 codewords
     t.s0 = (r / cw_waves) * a.M;
     t.s1 = min(t.s0 + a.M, a.nS);
     const int b_raw = t.cwv * 64 + (threadIdx.x & 63);
@@ -2433,6 +2467,14 @@ __device__ __forceinline__ void sw_lut_fill(T* lut_s, const DecodeParams<T>& p)
     __syncthreads();
 }
 
+// a use of v that the compiler must wait for (s_waitcnt on its load) before anything after this
+// statement, memory operations included
+template <typename T>
+__device__ __forceinline__ void sw_wait_on(const T& v)
+{
+    asm volatile("" ::"v"(v) : "memory");
+}
+
 __device__ __forceinline__ int sw_end(int s, int nS, int W, int L) { return s == nS - 1 ? L : (s + 1) * W; }
 __device__ __forceinline__ int floor_div(int x, int m) { return x >= 0 ? x / m : -((-x + m - 1) / m); }
 
@@ -2443,8 +2485,16 @@ __device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s,
 }
 
 // ---- alpha: forward over the run, checkpoints every S positions of each sub-block
+#ifndef TD_SW_ALPHA_WAVES
+#define TD_SW_ALPHA_WAVES 0
+#endif
+#if TD_SW_ALPHA_WAVES
+#define TD_SW_ALPHA_ATTR __attribute__((amdgpu_waves_per_eu(TD_SW_ALPHA_WAVES)))
+#else
+#define TD_SW_ALPHA_ATTR
+#endif
 template <typename T, int ALGO, int S>
-__global__ __launch_bounds__(256) void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
+__global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ T lut_s[kLutElems<T>];
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
@@ -2498,44 +2548,81 @@ __global__ __launch_bounds__(256) void sw_alpha_kernel(DecodeParams<T> p, WinArg
 #pragma unroll
     for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, bp + m);
     for (; bp <= stop; bp += S) {
-        SwRaw<T> cx[S];
+        // the segment's inputs from the prefetch registers, then the next segment's loads into them
+        // (converting first keeps one copy of them live: no register moves at the loop edge)
+        SwIn<T> x[S];
 #pragma unroll
-        for (int m = 0; m < S; ++m) {
-            cx[m] = nx[m];
-            nx[m] = sw_raw(p, a, dec, b, bp + S + m);   // next segment, one segment ahead
-        }
+        for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
 #pragma unroll
-        for (int m = 0; m < S; ++m) {
-            const int pos = bp + m;
-            if (pos < ps || pos > stop) continue;
-            if (m == 0 && pos >= st && pos < en) {       // checkpoint alpha[pos] (normalised)
-                T* ck = sw_ck(a, t, s, (pos - st) / S);
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, bp + S + m);
+        // Fast segments (all but about one in eight): whole, no chain start or NII position inside, each
+        // chain stepping at every position or at none -- one straight block, the two chains' max*
+        // interleaved.  The others take the per-position path below.
+        const bool qin = (hasB || s < nS - 1) && qb >= bp && qb < bp + S;
+        const bool aAll = bp + S <= need, aNone = bp >= need;
+        const bool bAll = hasB && bp > qb, bNone = !hasB || bp + S <= qb;
+        if (bp >= ps && bp + S - 1 <= stop && !qin && (aAll || aNone) && (bAll || bNone) && !(aNone && bNone)) {
+            if (bp >= st) {                               // checkpoint alpha[bp] (normalised)
+                T* ck = sw_ck(a, t, s, (bp - st) / S);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) ck[j * 64] = al[j];
             }
-            if (s < nS - 1 && pos == qb && t.live)
+            if (aAll && bAll) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
-            if (hasB && pos == qb) {                     // sub-block s+1's chain starts here
-                if (qb <= 0)
-                    sw_set(bl, 1, (T)0);
-                else if (use_nii)
+                for (int m = 0; m < S; ++m) {
+                    sw_alpha_step2<T, ALGO>(al, bl, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(al);
+                sw_normalise(bl);
+            } else if (aAll) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
-                else
-                    sw_set(bl, 0, (T)0);
+                for (int m = 0; m < S; ++m) {
+                    sw_alpha_step<T, ALGO>(al, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(al);
+            } else {
+#pragma unroll
+                for (int m = 0; m < S; ++m) {
+                    sw_alpha_step<T, ALGO>(bl, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(bl);
             }
-            const SwIn<T> x = sw_cvt(cx[m], pos < a.la_len);
-            const bool doA = pos < need, doB = hasB && pos >= qb;
-            if (doA && doB)
-                sw_alpha_step2<T, ALGO>(al, bl, x, lut);
-            else if (doA)
-                sw_alpha_step<T, ALGO>(al, x, lut);
-            else if (doB)
-                sw_alpha_step<T, ALGO>(bl, x, lut);
-            if (m == S - 1) {                            // alpha[bp + S]: an aligned position
-                if (doA) sw_normalise(al);
-                if (doB) sw_normalise(bl);
+        } else {
+#pragma unroll
+            for (int m = 0; m < S; ++m) {
+                const int pos = bp + m;
+                if (pos < ps || pos > stop) continue;
+                if (m == 0 && pos >= st && pos < en) {       // checkpoint alpha[pos] (normalised)
+                    T* ck = sw_ck(a, t, s, (pos - st) / S);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ck[j * 64] = al[j];
+                }
+                if (s < nS - 1 && pos == qb && t.live)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
+                if (hasB && pos == qb) {                     // sub-block s+1's chain starts here
+                    if (qb <= 0)
+                        sw_set(bl, 1, (T)0);
+                    else if (use_nii)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
+                    else
+                        sw_set(bl, 0, (T)0);
+                }
+                const bool doA = pos < need, doB = hasB && pos >= qb;
+                if (doA && doB)
+                    sw_alpha_step2<T, ALGO>(al, bl, x[m], lut);
+                else if (doA)
+                    sw_alpha_step<T, ALGO>(al, x[m], lut);
+                else if (doB)
+                    sw_alpha_step<T, ALGO>(bl, x[m], lut);
+                if (m == S - 1) {                            // alpha[bp + S]: an aligned position
+                    if (doA) sw_normalise(al);
+                    if (doB) sw_normalise(bl);
+                }
             }
         }
         if (hasB && bp + S == en) {                      // hand over to sub-block s+1
@@ -2557,11 +2644,20 @@ __global__ __launch_bounds__(256) void sw_alpha_kernel(DecodeParams<T> p, WinArg
 }
 
 // ---- beta + LLR: backward over the run in segments of S positions
+#ifndef TD_SW_BETA_WAVES
+#define TD_SW_BETA_WAVES 0
+#endif
+#if TD_SW_BETA_WAVES
+#define TD_SW_BETA_ATTR __attribute__((amdgpu_waves_per_eu(TD_SW_BETA_WAVES)))
+#else
+#define TD_SW_BETA_ATTR
+#endif
 template <typename T, int ALGO, int S>
-__global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
+__global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
                                                       const int* __restrict__ pinv)
 {
     __shared__ T lut_s[kLutElems<T>];
+    __shared__ alignas(16) T ck_lds[4 * 8 * 64];   // per wave: the next segment's checkpoint (DMA slot)
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
@@ -2573,7 +2669,7 @@ __global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs
     const bool use_nii = a.nii && a.it > 0;
     const int base0 = t.s0 * W;
     const int* const perm = dec ? pi : pinv;
-    T* const le = a.le[dec] + (size_t)(b >> 3) * K * kCw + (b & 7);
+    T* const le = a.le[dec] + (size_t)(b >> 6) * K * kSwCw + (b & 63);
     uint8_t* const bitsT = dec ? a.bitsT : nullptr;
     const int bcol = t.cwv * 64 + lane;
 
@@ -2603,60 +2699,80 @@ __global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs
         for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = j == 0 ? (T)0 : (T)-kInfty;
     const int pe = min(e, L) - 1;                 // first position stepped
 
-    // segment prefetch: inputs and, for a segment of a sub-block's own range, its checkpoint
+    // Segment prefetch, one segment ahead: the inputs into registers and, for a segment of a sub-block's
+    // own range, its checkpoint (8 x 64 lane-contiguous values) into this wave's LDS slot by DMA
+    // (global_load_lds_dwordx4: no VGPR holds it in flight; in registers, with the merge of the
+    // segments that have none, it cost 46 VGPRs).  The DMA is issued BEFORE the input loads: VMEM loads
+    // complete in order, so once the compiler's wait for the first input load is past (sw_wait_on),
+    // the checkpoint has landed.  The slot is rewritten only after its reads (lgkmcnt(0)).
     auto seg_sub = [&](int sbp) {                 // sub-block whose chain covers segment sbp
         return sbp >= en ? s : min(t.s0 + (sbp - base0) / W, t.s1 - 1);
     };
+    T* const ckslot = ck_lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 8 * 64;
+    const unsigned ckslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(ckslot));   // DMA base (M0): wave-uniform
     int bp = base0 + floor_div(pe - base0, S) * S;
     SwRaw<T> nx[S];
-    T nck[8] = {};
     auto prefetch = [&](int nbp) {
-#pragma unroll
-        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, nbp + m);
         const int ns = seg_sub(nbp), nst = ns * W;
         if (nbp >= base0 && nbp < sw_end(ns, nS, W, L)) {
-            const T* ck = sw_ck(a, t, ns, (nbp - nst) / S);
+            const char* src = reinterpret_cast<const char*>(sw_ck(a, t, ns, (nbp - nst) / S) - lane) + lane * 16;
+            constexpr int kDma = 8 * 64 * (int)sizeof(T) / 1024;   // 1 KB per wave instruction
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // the slot's previous reads are done
 #pragma unroll
-            for (int j = 0; j < 8; ++j) nck[j] = ck[j * 64];
+            for (int q = 0; q < kDma; ++q) dma16(ckslot_lds + q * 1024, src + q * 1024);
         }
+#pragma unroll
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, nbp + m);
     };
     prefetch(bp);
+    // one position's LLR, extrinsic and decision (beta = beta[pos + 1]); `live`: the generic path's
+    // stores skip the padding lanes (the fast path lets them store: they decode codeword B-1 again
+    // and write its own values to its own addresses, or to their own unused bitsT columns)
+    auto llr_out = [&](int pos, const T (&al)[8], const SwIn<T>& xm, bool live) {
+        const T llr = sw_llr<T, ALGO>(al, be, xm, lut);
+        const T lev = (llr - xm.la - (T)2 * xm.ys) * a.ext_scale;
+        if (live) {
+            if (pos < K) {
+                le[(size_t)perm[pos] * kSwCw] = lev;
+                if (bitsT) bitsT[(size_t)pi[pos] * a.Bp + bcol] = llr < (T)0 ? 0 : 1;
+            }
+            if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
+        }
+    };
     for (; bp >= base0; bp -= S) {
-        SwRaw<T> cx[S];
-        T as[S][8];
-#pragma unroll
-        for (int m = 0; m < S; ++m) cx[m] = nx[m];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) as[0][j] = nck[j];
-        if (bp - S >= base0) prefetch(bp - S);
         SwIn<T> x[S];
-#pragma unroll
-        for (int m = 0; m < S; ++m) x[m] = sw_cvt(cx[m], bp + m < a.la_len);
+        T as[S][8];
         const bool main = bp < en;                        // the segment lies in sub-block s's own range
+        sw_wait_on(nx[0].ys);                             // this segment's inputs, and its checkpoint DMA, landed
+#pragma unroll
+        for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
+        if (main)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) as[0][j] = ckslot[j * 64 + lane];
+        if (bp - S >= base0) prefetch(bp - S);
         if (main) {                                       // alpha of the segment from its checkpoint
 #pragma unroll
-            for (int m = 1; m < S; ++m) {
+            for (int m = 1; m < S; ++m) {                 // (past en in the last segment: computed, unused)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) as[m][j] = as[m - 1][j];
-                if (bp + m < en) sw_alpha_step<T, ALGO>(as[m], x[m - 1], lut);
+                sw_alpha_step<T, ALGO>(as[m], x[m - 1], lut);
+                sw_fence();
             }
         }
-#pragma unroll
-        for (int m = S - 1; m >= 0; --m) {
-            const int pos = bp + m;
-            if (pos > pe) continue;
-            if (main && pos < en) {                       // LLR, extrinsic, decision (beta = beta[pos + 1])
-                const T llr = sw_llr<T, ALGO>(as[m], be, x[m], lut);
-                const T lev = (llr - x[m].la - (T)2 * x[m].ys) * a.ext_scale;
-                if (t.live) {
-                    if (pos < K) {
-                        le[(size_t)perm[pos] * kCw] = lev;
-                        if (bitsT) bitsT[(size_t)pi[pos] * a.Bp + bcol] = llr < (T)0 ? 0 : 1;
-                    }
-                    if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
-                }
-            }
-            if (hasB && pos == qb - 1) {                  // sub-block s-1's chain starts at qb
+        // Fast segments: whole, every position in sub-block s's range (below K) or every one past it,
+        // no chain start strictly inside and no NII position, s-1's chain stepping everywhere or nowhere
+        const int nb = st + g;                            // NII beta position of s-1
+        const bool whole = bp + S - 1 <= pe;
+        const bool allMain = bp + S <= en && bp + S <= K, noMain = bp >= en;
+        const bool binit_top = hasB && qb - 1 == bp + S - 1;
+        const bool bin = hasB && qb - 1 >= bp && qb - 1 < bp + S - 1;
+        const bool nbin = s > 0 && nb >= bp && nb < bp + S;
+        const bool bAll = hasB && bp + S - 1 < qb, bNone = !hasB || bp >= qb;
+#ifndef TD_SW_BETA_FAST
+#define TD_SW_BETA_FAST 0   // straight-line fast segments in the beta kernel (286 VGPRs: measured slower)
+#endif
+        if (TD_SW_BETA_FAST && whole && (allMain || noMain) && !bin && !nbin && (bAll || bNone)) {
+            if (binit_top) {                              // sub-block s-1's chain starts at qb = bp + S
                 if (qb >= L)
                     sw_set(bb, 1, (T)0);
                 else if (use_nii)
@@ -2665,18 +2781,67 @@ __global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs
                 else
                     sw_set(bb, 0, (T)0);
             }
-            const bool doB = hasB && pos < qb;
-            if (doB)
-                sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
-            else
-                sw_beta_step<T, ALGO>(be, x[m], lut);
-            if (m == 0) {                                 // beta[bp]: an aligned position
-                sw_normalise(be);
-                if (doB) sw_normalise(bb);
-            }
-            if (s > 0 && pos == st + g && t.live)
+            if (allMain && bAll) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
+                for (int m = S - 1; m >= 0; --m) {
+                    llr_out(bp + m, as[m], x[m], true);
+                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(be);
+                sw_normalise(bb);
+            } else if (allMain) {
+#pragma unroll
+                for (int m = S - 1; m >= 0; --m) {
+                    llr_out(bp + m, as[m], x[m], true);
+                    sw_beta_step<T, ALGO>(be, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(be);
+            } else if (bAll) {
+#pragma unroll
+                for (int m = S - 1; m >= 0; --m) {
+                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(be);
+                sw_normalise(bb);
+            } else {
+#pragma unroll
+                for (int m = S - 1; m >= 0; --m) {
+                    sw_beta_step<T, ALGO>(be, x[m], lut);
+                    sw_fence();
+                }
+                sw_normalise(be);
+            }
+        } else {
+#pragma unroll
+            for (int m = S - 1; m >= 0; --m) {
+                const int pos = bp + m;
+                if (pos > pe) continue;
+                if (main && pos < en) llr_out(pos, as[m], x[m], t.live);
+                if (hasB && pos == qb - 1) {              // sub-block s-1's chain starts at qb
+                    if (qb >= L)
+                        sw_set(bb, 1, (T)0);
+                    else if (use_nii)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
+                    else
+                        sw_set(bb, 0, (T)0);
+                }
+                const bool doB = hasB && pos < qb;
+                if (doB)
+                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
+                else
+                    sw_beta_step<T, ALGO>(be, x[m], lut);
+                if (m == 0) {                             // beta[bp]: an aligned position
+                    sw_normalise(be);
+                    if (doB) sw_normalise(bb);
+                }
+                if (s > 0 && pos == nb && t.live)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
+            }
         }
         if (hasB && bp == st) {                           // hand over to sub-block s-1
             if (qb <= st) {                               // g = 0: its chain starts at its end
@@ -2694,6 +2859,61 @@ __global__ __launch_bounds__(256) void sw_beta_kernel(DecodeParams<T> p, WinArgs
                 for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
         }
     }
+}
+
+// Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the stream [B][3K+12] into the windowed
+// schedule's wide arrays.  A block transposes 64 codewords x kSwDemuxSteps steps through LDS: each
+// codeword's 3 x 16 values are one contiguous 384-byte piece of its row, each output row is 512
+// bytes.  SISO2's systematic input (sys1 at pi, :1109-1113) is written in the same pass, row i of
+// sys1 going to sys2 row pinv(i), so no gather follows (the 8-codeword layout needs demux_perm_kernel).
+// The last x-block writes the three tail steps of both encoders (:1119-1123).
+constexpr int kSwDemuxSteps = 16;
+template <typename T>
+__global__ __launch_bounds__(256) void sw_demux_kernel(DecodeParams<T> p, const T* __restrict__ flow)
+{
+    __shared__ T tile[kSwCw][3 * kSwDemuxSteps + 1];
+    const int K = p.K, L = p.L, n = 3 * K + 4 * kMemory;
+    const int gw = blockIdx.y, i0 = blockIdx.x * kSwDemuxSteps;
+    const T h = (T)0.5;
+    if (i0 >= K) {   // the tail block: steps K .. K+2 of the four streams
+        for (int e = threadIdx.x; e < kSwCw * kMemory; e += blockDim.x) {
+            const int c = e & 63, j = e >> 6, b = gw * kSwCw + c;
+            T v[4] = {0, 0, 0, 0};
+            if (b < p.B)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = flow[(size_t)b * n + 3 * K + (u >> 1) * 2 * kMemory + 2 * j + (u & 1)] * h;
+            const size_t off = ((size_t)gw * L + K + j) * kSwCw + c;
+            p.sys1[off] = v[0];
+            p.par1[off] = v[1];
+            p.sys2[off] = v[2];
+            p.par2[off] = v[3];
+        }
+        return;
+    }
+    const int ns = min(kSwDemuxSteps, K - i0);
+    for (int e = threadIdx.x; e < kSwCw * 3 * kSwDemuxSteps; e += blockDim.x) {
+        const int c = e / (3 * kSwDemuxSteps), q = e % (3 * kSwDemuxSteps), b = gw * kSwCw + c;
+        tile[c][q] = (b < p.B && q < 3 * ns) ? flow[(size_t)b * n + 3 * i0 + q] * h : (T)0;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kSwCw * ns; e += blockDim.x) {
+        const int c = e & 63, k = e >> 6, i = i0 + k;
+        const size_t row = (size_t)gw * L;
+        const T ys = tile[c][3 * k];
+        p.sys1[(row + i) * kSwCw + c] = ys;
+        p.par1[(row + i) * kSwCw + c] = tile[c][3 * k + 1];
+        p.par2[(row + i) * kSwCw + c] = tile[c][3 * k + 2];
+        p.sys2[(row + p.pinv[i]) * kSwCw + c] = ys;
+    }
+}
+
+template <typename T>
+hipError_t launch_window_demux(const DecodeParams<T>& p, const T* flow, hipStream_t st)
+{
+    const int Bp = (p.B + kSwCw - 1) / kSwCw * kSwCw;
+    hipLaunchKernelGGL(sw_demux_kernel<T>, dim3((p.K + kSwDemuxSteps - 1) / kSwDemuxSteps + 1, Bp / kSwCw), dim3(256),
+                       0, st, p, flow);
+    return hipGetLastError();
 }
 
 // SISO2's decisions [K][Bp] (rows in natural order) -> bits [B][K] (row stride `stride`): 64 x 64-byte
@@ -2748,8 +2968,21 @@ int window_run(int L, int W, int g, int B, int ndec, int S, int force)
     return m < 1 ? 1 : (m > nS ? nS : (int)m);
 }
 
+// Two halves of the batch on two streams (round 5).  The alpha kernel streams inputs and checkpoints
+// (HBM-heavy, light VALU) and the beta kernel is VALU- and LDS-heavy with light traffic; back to back on
+// one stream each leaves the other resource idle.  The halves are independent codewords, so half B runs
+// on a second stream one alpha launch behind half A, and the GPU co-schedules one half's alpha with the
+// other's beta.  Used when each half keeps at least kSwHalfWaves waves of 64 codewords and a second
+// stream is given (td_api.cpp); SISO2's decisions of every wanted iteration are transposed after the
+// join (all_iters decodes keep one stream: their per-iteration transposes would re-join the halves).
+#ifndef TD_SW_HALF_WAVES
+#define TD_SW_HALF_WAVES 64
+#endif
+constexpr int kSwHalfWaves = TD_SW_HALF_WAVES;
+
 template <typename T, int ALGO>
-hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)
+hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st,
+                              const WindowStreams& ws)
 {
     constexpr int S = sw_seg<T>();
     const int W = w.window;
@@ -2759,8 +2992,6 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.W = W;
     a.g = w.overlap;
     a.nS = nS;
-    a.M = window_run(p.L, W, w.overlap, p.B, ndec, S, w.run);
-    a.nR = (nS + a.M - 1) / a.M;
     a.Bp = (p.B + 63) / 64 * 64;
     a.ncp = (p.L - (nS - 1) * W + S - 1) / S;
     a.ext_scale = (T)w.ext_scale;
@@ -2768,8 +2999,24 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.ckpt[0] = wb.ckpt[0];
     a.ckpt[1] = wb.ckpt[1];
     const size_t nii_half = (size_t)2 * p.B * nS * 16;
-    const long long waves = (long long)a.nR * (a.Bp / 64) * ndec;
-    const int blocks = (int)((waves + 3) / 4);
+    const int cw_total = a.Bp / 64;
+    const bool split = ws.st2 && !p.all_iters && cw_total >= 2 * kSwHalfWaves;
+    const int nparts = split ? 2 : 1;
+    struct Part {
+        int cw0, ncw, M, nR, blocks;
+        hipStream_t s;
+    } part[2];
+    for (int h = 0; h < nparts; ++h) {
+        Part& q = part[h];
+        q.cw0 = h == 0 ? 0 : cw_total / 2;
+        q.ncw = nparts == 1 ? cw_total : (h == 0 ? cw_total / 2 : cw_total - cw_total / 2);
+        q.M = window_run(p.L, W, w.overlap, q.ncw * 64, ndec, S, w.run);
+        q.nR = (nS + q.M - 1) / q.M;
+        q.blocks = (int)(((long long)q.nR * q.ncw * ndec + 3) / 4);
+        q.s = h == 0 ? st : ws.st2;
+    }
+    auto check = [] { return hipGetLastError(); };
+    bool forked = false;
     for (int it = 0; it < p.iters; ++it) {
         a.it = it;
         a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
@@ -2790,18 +3037,43 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 a.la[0] = a.le[1] = wb.ext21[0];
                 a.la[1] = a.le[0] = wb.ext12[0];
             }
-            hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a);
-            hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S>), dim3(blocks), dim3(256), 0, st, p, a, p.pi, p.pinv);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+            for (int h = 0; h < nparts; ++h) {
+                const Part& q = part[h];
+                a.cw0 = q.cw0;
+                a.ncw = q.ncw;
+                a.M = q.M;
+                a.nR = q.nR;
+                if (h == 1 && !forked) {   // half B starts one alpha launch behind half A
+                    hipError_t e = hipStreamWaitEvent(q.s, ws.fork, 0);
+                    if (e != hipSuccess) return e;
+                    forked = true;
+                }
+                hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocks), dim3(256), 0, q.s, p, a);
+                if (h == 0 && split && !forked) {
+                    hipError_t e = hipEventRecord(ws.fork, q.s);
+                    if (e != hipSuccess) return e;
+                }
+                hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S>), dim3(q.blocks), dim3(256), 0, q.s, p, a, p.pi, p.pinv);
+                hipError_t e = check();
+                if (e != hipSuccess) return e;
+            }
         }
-        if (want_bits) {
+        if (want_bits && (p.all_iters || !split)) {
             const long long stride = p.all_iters ? (long long)p.iters * p.K : p.K;
             hipLaunchKernelGGL(bits_transpose_kernel, dim3((p.K + 63) / 64, a.Bp / 64), dim3(256), 0, st, wb.bitsT,
                                p.K, a.Bp, p.B, p.bits + (p.all_iters ? (size_t)it * p.K : 0), stride);
-            hipError_t e = hipGetLastError();
+            hipError_t e = check();
             if (e != hipSuccess) return e;
         }
+    }
+    if (split) {   // join half B back into the caller's stream, then the decisions
+        hipError_t e = hipEventRecord(ws.join, ws.st2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ws.join, 0);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(bits_transpose_kernel, dim3((p.K + 63) / 64, a.Bp / 64), dim3(256), 0, st, wb.bitsT, p.K,
+                           a.Bp, p.B, p.bits, (long long)p.K);
+        e = check();
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
@@ -2817,9 +3089,10 @@ size_t window_ckpt_elems(int B, int L, int W, bool f32)
 size_t window_bits_bytes(int B, int K) { return (size_t)K * ((B + 63) / 64) * 64; }
 
 template <typename T>
-hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st)
+hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st,
+                         const WindowStreams& ws)
 {
-    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st) : launch_window_algo<T, 0>(p, w, wb, st);
+    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st, ws) : launch_window_algo<T, 0>(p, w, wb, st, ws);
 }
 
 constexpr int kDemuxBlocks = 32768;   // grid cap of demux_kernel (grid-stride loop beyond); 8192: 0.230 ms, 32768: 0.212 (config 2)
@@ -3069,12 +3342,14 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
 
 #ifndef TD_W12_TU
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
+template hipError_t launch_window_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
+template hipError_t launch_window_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t, bool);
 template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, const WindowBufs<double>&,
-                                         hipStream_t);
+                                         hipStream_t, const WindowStreams&);
 template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, const WindowBufs<float>&,
-                                        hipStream_t);
+                                        hipStream_t, const WindowStreams&);
 template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t, bool);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);
