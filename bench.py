@@ -159,7 +159,7 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
                     "traffic_frac": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic_frac_measured_ceiling": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_MEASURED_GBS, 4),
                     "valu_instr_per_decode": int(vi), "valu_issue_frac": round(vi / cap, 4),
-                    "sclk_ghz": round(clk, 4), "sclk_source": "power record (amdsmi)" if sclk_ghz else "constant",
+                    "sclk_ghz": round(clk, 4), "sclk_source": "measured (td_clock_read: one beta workgroup)" if sclk_ghz else "constant",
                     "pmc_source": rec.get("source"), "kernel": rec.get("kernel")})
     return out
 
@@ -224,11 +224,11 @@ def main():
     demux_ms, turbo_ms, nlaunch = codec.kernel_ms()
     codec.profile(False)
     clock = None
-    if not a.window:   # the last launch's sustained shader clock (td_clock_read), outside the timed region
-        try:
-            clock = codec.clock()
-        except Exception:
-            clock = None
+    # the last launch's sustained shader clock (td_clock_read; windowed: one beta workgroup), outside the timed region
+    try:
+        clock = codec.clock()
+    except Exception:
+        clock = None
 
     errs = int((bits != u_d).sum().item())
     blk = int((bits != u_d).any(dim=1).sum().item())
@@ -613,7 +613,7 @@ def summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2,
             "kernel_ms_avg": round(turbo_ms, 4),
             "demux_ms_avg": round(demux_ms, 4),
             "launches_timed": nlaunch,
-            "window": (window_roofline(a.K, a.batch, a.iters, demux_ms + turbo_ms)
+            "window": (window_roofline(a.K, a.batch, a.iters, demux_ms + turbo_ms, sclk)
                        if a.window and a.precision == "f64" and a.algo == "logmap" and turbo_ms > 0 else None),
         },
         "ber": {"bit_errors": errs, "block_errors": blk,
@@ -795,6 +795,10 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         _, kms, _ = c.kernel_ms()
+        try:
+            vclk = c.clock()[0]
+        except Exception:
+            vclk = None
         c.close()
         errs = int((b != ub).sum().item())
         del x
@@ -804,7 +808,7 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B, "config": cfg,
                     "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
         if win and prec == "f64" and algo == "logmap":
-            res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3)
+            res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3, vclk)
     if big is not None and a.K == 6144:
         res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
     return res

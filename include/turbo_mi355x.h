@@ -131,9 +131,11 @@ int td_profile_enable(td_handle* h, int on);
 int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launches);
 /* Launch clock (measurement support): every exact-schedule turbo launch records, in its first
  * workgroup, the shader clock (s_memtime) and the 100 MHz real-time counter (s_memrealtime) at that
- * workgroup's start and end.  td_clock_read waits for this handle's last decode (not the whole
- * device) and returns that launch's sustained shader clock (GHz) and the workgroup's span (ms);
- * TD_EINVAL before any such launch or when the last decode was windowed or graph-captured. */
+ * workgroup's start and end; a windowed decode records the same in the first workgroup of its
+ * last SISO2 beta launch (round 5).  td_clock_read waits for this handle's last decode (not the
+ * whole device) and returns the sustained shader clock (GHz) over that workgroup's span (ms: the
+ * whole launch for the exact schedule, one workgroup's lifetime for a windowed one);
+ * TD_EINVAL before any decode or when the last decode was graph-captured. */
 int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms);
 
 /* Diagnostics: in a library built with -DTD_STAMPS (td_debug_stamp_slots() > 0) the turbo

@@ -165,6 +165,22 @@ def test_set_window_rejects_bad_arguments():
         c.set_window(0, 0, 1.0)
 
 
+@pytest.mark.parametrize("conc", [False, True])
+def test_window_launch_clock(conc):
+    """td_clock_read after a windowed decode (round 5): the first workgroup of the last SISO2 beta
+    launch samples the clock, so the config-5 roofline prices VALU issue at the launch's own clock."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2 = 1024, 31, 64
+    _, flow = O.synth_batch(K, f1, f2, 0.4, 91, 300)
+    with TurboCodec(K, f1, f2, iterations=2) as c:
+        c.set_window(64, 30, concurrent=conc)
+        c.decode(torch.from_numpy(flow).to("cuda:0"))
+        ghz, span = c.clock()
+        assert 0.5 < ghz < 3.0 and span > 0, (ghz, span)
+
+
 def test_reference_gpu_decoder_ber_matches_published():
     """The reference GPU decoder's schedule (P = 64 sub-blocks, NII, concurrent SISOs, Le x0.77,
     Max-Log-MAP fp32) at 10 iterations on 2000 of main.cpp's frames per point: BER and FER

@@ -61,8 +61,8 @@ struct td_handle {
     void* d_lut = nullptr;
     td::LaneTables* d_lane = nullptr;
     unsigned* d_slots = nullptr;   // per-CU occupancy bits of the turbo kernel (wg_pos)
-    unsigned long long* d_clk = nullptr;   // the last exact-schedule launch's clock samples (td_clock_read)
-    bool clk_exact = false;                // the last decode was an exact-schedule launch (d_clk is its sample)
+    unsigned long long* d_clk = nullptr;   // the last decode's clock sample (td_clock_read)
+    bool clk_valid = false;                // the last decode was eager (a captured one leaves no sample)
     // td_decode_host's device staging (input stream, bits, optional Le), grown on demand and kept: the
     // drop-in's TurboDecoding decodes one frame per call, so per-call allocations would be per frame
     void* d_hin = nullptr;
@@ -393,7 +393,7 @@ WinCarve win_carve(const td_handle* h, int B)
     const int K = h->p.K, L = K + td::kMemory, G = groups_for(B);
     WinCarve c{};
     c.arrK = align_up(((size_t)B + 63) / 64 * 64 * K * elem, 256);   // wide groups of 64 codewords
-    c.nii = (size_t)2 * 2 * B * td::window_subblocks(L, h->wp.window) * 16 * elem;
+    c.nii = (size_t)2 * 2 * (((size_t)B + 63) / 64 * 64) * td::window_subblocks(L, h->wp.window) * 16 * elem;
     c.arrC = align_up(td::window_ckpt_elems(B, L, h->wp.window, elem == 4) * elem, 256);
     c.nii = align_up(c.nii, 256);
     c.arrT = align_up(td::window_bits_bytes(B, K), 256);
@@ -515,7 +515,7 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     else
         e = td::launch_turbo<T>(dp, st);
     if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
-    h->clk_exact = !h->wp.window && !capturing;
+    h->clk_valid = !capturing;
     if (ev) {
         TD_HIP(hipEventRecord(ev[2], st));
         ++h->nev;
@@ -879,13 +879,13 @@ int td_profile_read(td_handle* h, float* demux_ms, float* decode_ms, int* launch
 int td_clock_read(td_handle* h, double* sclk_ghz, double* span_ms)
 {
     if (!h) return fail(TD_EINVAL, "td_clock_read: null handle");
-    if (!h->clk_exact) return fail(TD_EINVAL, "td_clock_read: the last decode was not an exact-schedule launch");
+    if (!h->clk_valid) return fail(TD_EINVAL, "td_clock_read: the last decode was captured into a graph");
     TD_HIP(hipSetDevice(h->p.device));
     if (h->ws_pending && h->ws_free) TD_HIP(hipEventSynchronize(h->ws_free));   // this handle's last decode only
     unsigned long long v[4] = {};
     TD_HIP(hipMemcpy(v, h->d_clk, sizeof v, hipMemcpyDeviceToHost));
     const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);   // s_memrealtime: 100 MHz
-    if (v[3] <= v[1] || v[2] <= v[0]) return fail(TD_EINVAL, "td_clock_read: no exact-schedule decode recorded yet");
+    if (v[3] <= v[1] || v[2] <= v[0]) return fail(TD_EINVAL, "td_clock_read: no decode recorded yet");
     if (sclk_ghz) *sclk_ghz = cyc / ticks * 0.1;
     if (span_ms) *span_ms = ticks * 1e-5;
     return TD_OK;

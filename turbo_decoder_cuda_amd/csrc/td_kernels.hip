@@ -2284,6 +2284,7 @@ struct WinArgs {
     T* nii_wr;
     T* ckpt[2];            // per decoder: [nS][Bp/64][ncp][8][64] alpha checkpoints
     uint8_t* bitsT;        // [K][Bp] SISO2's decisions (natural-order rows); null: none this launch
+    int clk;               // workgroup 0 of this beta launch samples the clock into p.clk (td_clock_read)
 };
 
 template <typename T>
@@ -2295,6 +2296,63 @@ struct SwRaw {
     T ys, yp, la;
 };
 
+// The windowed kernels' max* table (round 5): three tables (thr, vlo, vhi = vlo of the next bucket) of
+// [bucket][32 columns]; lane l reads column l % 32 of each with one ds_read_b64 at a common row
+// address, so the 32 lanes an LDS cycle serves hit 64 distinct banks whatever their buckets: 3 x 2 LDS
+// cycles a max*, conflict-free.  (The exact kernel's layout, a ds_read2_b64 and a ds_read_b64 on 16
+// columns, takes 8 + 2-4: SQ_LDS_BANK_CONFLICT was 15-16 % of the windowed kernels' LDS cycles with it.)
+// The tables sit an odd number of 8-byte words apart, more than 2040 B, so the compiler cannot merge
+// two reads into a ds_read2 / ds_read2st64 (4x16-lane groups on 32 banks).  The row address is the
+// same one lshl_add of the clamped bucket field as before.
+template <typename T>
+struct SwLut {
+    static constexpr int kCols = 32;
+    static constexpr int kRow = kCols * (int)sizeof(T);           // bytes per bucket row
+    static constexpr int kRows = kLutSize + 1;                     // + a pad row (clamped field)
+    static constexpr int kTab = kRows * kRow;
+    static constexpr int kOffV = kTab + (int)sizeof(T);
+    static constexpr int kOffH = 2 * kOffV + (int)sizeof(T);
+    static constexpr int kBytes = kOffH + kTab;
+};
+static_assert(SwLut<double>::kOffV % 512 && (SwLut<double>::kOffH - SwLut<double>::kOffV) % 512 &&
+                  SwLut<double>::kOffH % 512 && SwLut<double>::kOffV > 2040, "no ds_read2 merging");
+
+template <typename T>
+__device__ __forceinline__ void sw_lut_fill(char* lut_s, const DecodeParams<T>& p)
+{
+    using Lt = SwLut<T>;
+    for (int e = threadIdx.x; e < Lt::kRows * Lt::kCols; e += blockDim.x) {
+        const int q = e / Lt::kCols, o = q * Lt::kRow + (e % Lt::kCols) * (int)sizeof(T);
+        const LutEntry<T>& last = p.lut[kLutSize - 1];
+        *reinterpret_cast<T*>(lut_s + o) = q < kLutSize ? (T)p.lut[q].thr : (T)INFINITY;
+        *reinterpret_cast<T*>(lut_s + Lt::kOffV + o) = q < kLutSize ? (T)p.lut[q].vlo : (T)last.vhi;
+        *reinterpret_cast<T*>(lut_s + Lt::kOffH + o) = q < kLutSize ? (T)p.lut[q].vhi : (T)last.vhi;
+    }
+    __syncthreads();
+}
+// this lane's table origin: its column, shifted down by the first bucket's field value
+template <typename T>
+__device__ __forceinline__ const char* sw_lut_lane(const char* lut_s, int lane)
+{
+    return lut_s + (lane % SwLut<T>::kCols) * (int)sizeof(T) - BucketBits<T>::base * SwLut<T>::kRow;
+}
+// E_algorithm (log_map.cpp:779-801) in the exact bucket form of mstar, on the windowed table
+template <typename T, int ALGO>
+__device__ __forceinline__ T sw_mstar(T x, T y, const char* lut)
+{
+    if constexpr (ALGO == 1) {
+        return vmax(x, y);
+    } else {
+        using Lt = SwLut<T>;
+        const T d = y - x;
+        const char* r = lut + bucket_dev<T>(d) * Lt::kRow;
+        const T thr = *reinterpret_cast<const T*>(r);
+        const T lo = *reinterpret_cast<const T*>(r + Lt::kOffV);
+        const T hi = *reinterpret_cast<const T*>(r + Lt::kOffH);
+        return vmax(x, y) + (fabs(d) >= thr ? hi : lo);
+    }
+}
+
 // The windowed schedule's arrays are WIDE (round 5): [B/64][L][64] and [B/64][K][64], the 64 codewords
 // of a wave adjacent per step, so a wave's load of one step is one 512-byte row (4 whole cache lines)
 // and its extrinsic store one 512-byte row at the interleaved position.  (The exact schedule keeps its
@@ -2302,15 +2360,19 @@ struct SwRaw {
 // 64-byte pieces per wave load, half a cache line each.
 constexpr int kSwCw = 64;
 // channel + a-priori of (codeword b, step i) of decoder `dec` (steps outside [0, L) clamped)
+// A wave's 64 codewords are the wide group cwv (wave-uniform) and its lanes, so every address is a
+// wave-uniform base plus the lane: no per-lane 64-bit pointer stays live across the loops (with the
+// codeword index per lane the compiler hoisted one per array and the beta kernel spilled into AGPRs).
 template <typename T>
-__device__ __forceinline__ SwRaw<T> sw_raw(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int b, int i)
+__device__ __forceinline__ SwRaw<T> sw_raw(const DecodeParams<T>& p, const WinArgs<T>& a, int dec, int cwv, int lane,
+                                          int i)
 {
     const int ic = min(max(i, 0), p.L - 1);
-    const size_t off = ((size_t)(b >> 6) * p.L + ic) * kSwCw + (b & 63);
+    const size_t row = (size_t)cwv * p.L + ic, rowk = (size_t)cwv * p.K + min(ic, p.K - 1);
     SwRaw<T> r;
-    r.ys = (dec ? p.sys2 : p.sys1)[off];
-    r.yp = (dec ? p.par2 : p.par1)[off];
-    r.la = a.la[dec][((size_t)(b >> 6) * p.K + min(ic, p.K - 1)) * kSwCw + (b & 63)];
+    r.ys = (dec ? p.sys2 : p.sys1)[row * kSwCw + lane];
+    r.yp = (dec ? p.par2 : p.par1)[row * kSwCw + lane];
+    r.la = a.la[dec][rowk * kSwCw + lane];
     return r;
 }
 // the step's P, Q (see "gamma") with La zero where no extrinsic exists (la_ok: i < la_len)
@@ -2340,27 +2402,27 @@ __device__ __forceinline__ void sw_normalise(T (&v)[8])
 
 // alpha[.][i] -> alpha[.][i+1] (log_map.cpp:975-985)
 template <typename T, int ALGO>
-__device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const T* lut)
+__device__ __forceinline__ void sw_alpha_step(T (&a)[8], const SwIn<T>& x, const char* lut)
 {
     T n[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
-        n[j] = mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
+        n[j] = sw_mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = n[j];
 }
 // two independent chains on the same step: one code block, so their 16 max* interleave
 template <typename T, int ALGO>
-__device__ __forceinline__ void sw_alpha_step2(T (&a)[8], T (&c)[8], const SwIn<T>& x, const T* lut)
+__device__ __forceinline__ void sw_alpha_step2(T (&a)[8], T (&c)[8], const SwIn<T>& x, const char* lut)
 {
     T n[8], m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
-        n[j] = mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
-        m[j] = mstar<T, ALGO>(c[p0] - sw_g(x, p0), c[p1] + sw_g(x, p1), lut);
+        n[j] = sw_mstar<T, ALGO>(a[p0] - sw_g(x, p0), a[p1] + sw_g(x, p1), lut);
+        m[j] = sw_mstar<T, ALGO>(c[p0] - sw_g(x, p0), c[p1] + sw_g(x, p1), lut);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2371,26 +2433,26 @@ __device__ __forceinline__ void sw_alpha_step2(T (&a)[8], T (&c)[8], const SwIn<
 
 // beta[.][i+1] -> beta[.][i] (log_map.cpp:1004-1016)
 template <typename T, int ALGO>
-__device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const T* lut)
+__device__ __forceinline__ void sw_beta_step(T (&b)[8], const SwIn<T>& x, const char* lut)
 {
     T n[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const T G = sw_g(x, j);
-        n[j] = mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
+        n[j] = sw_mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[j] = n[j];
 }
 template <typename T, int ALGO>
-__device__ __forceinline__ void sw_beta_step2(T (&b)[8], T (&c)[8], const SwIn<T>& x, const T* lut)
+__device__ __forceinline__ void sw_beta_step2(T (&b)[8], T (&c)[8], const SwIn<T>& x, const char* lut)
 {
     T n[8], m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const T G = sw_g(x, j);
-        n[j] = mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
-        m[j] = mstar<T, ALGO>(c[kTrellisNext[j][0]] - G, c[kTrellisNext[j][1]] + G, lut);
+        n[j] = sw_mstar<T, ALGO>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
+        m[j] = sw_mstar<T, ALGO>(c[kTrellisNext[j][0]] - G, c[kTrellisNext[j][1]] + G, lut);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2412,7 +2474,7 @@ __device__ __forceinline__ void sw_fence()
 
 // LLR of step i (log_map.cpp:1024-1039): the two left folds of E over the 8 next states
 template <typename T, int ALGO>
-__device__ __forceinline__ T sw_llr(const T (&a)[8], const T (&b)[8], const SwIn<T>& x, const T* lut)
+__device__ __forceinline__ T sw_llr(const T (&a)[8], const T (&b)[8], const SwIn<T>& x, const char* lut)
 {
     T t0[8], t1[8];
 #pragma unroll
@@ -2421,11 +2483,11 @@ __device__ __forceinline__ T sw_llr(const T (&a)[8], const T (&b)[8], const SwIn
         t0[j] = (a[p0] - sw_g(x, p0)) + b[j];
         t1[j] = (a[p1] + sw_g(x, p1)) + b[j];
     }
-    T r0 = mstar<T, ALGO>(t0[0], t0[1], lut), r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
+    T r0 = sw_mstar<T, ALGO>(t0[0], t0[1], lut), r1 = sw_mstar<T, ALGO>(t1[0], t1[1], lut);
 #pragma unroll
     for (int j = 2; j < 8; ++j) {
-        r0 = mstar<T, ALGO>(r0, t0[j], lut);
-        r1 = mstar<T, ALGO>(r1, t1[j], lut);
+        r0 = sw_mstar<T, ALGO>(r0, t0[j], lut);
+        r1 = sw_mstar<T, ALGO>(r1, t1[j], lut);
     }
     return r1 - r0;
 }
@@ -2454,18 +2516,13 @@ __device__ __forceinline__ bool sw_task(const DecodeParams<T>& p, const WinArgs<
     t.cwv = a.cw0 + r % cw_waves;   // absolute wave of 64 codewords
     t.s0 = (r / cw_waves) * a.M;
     t.s1 = min(t.s0 + a.M, a.nS);
-    const int b_raw = t.cwv * 64 + (threadIdx.x & 63);
-    t.live = b_raw < p.B;
-    t.b = t.live ? b_raw : p.B - 1;
+    // padding lanes (b >= B) decode the zeros the demux wrote for them: every array they store to is
+    // sized for whole waves (Bp), and only the Le dump, sized B, skips them
+    t.b = t.cwv * 64 + (threadIdx.x & 63);
+    t.live = t.b < p.B;
     return true;
 }
 
-template <typename T>
-__device__ __forceinline__ void sw_lut_fill(T* lut_s, const DecodeParams<T>& p)
-{
-    for (int e = threadIdx.x; e < kLutElems<T>; e += blockDim.x) lut_s[e] = lut_elem<T>(p.lut, e);
-    __syncthreads();
-}
 
 // a use of v that the compiler must wait for (s_waitcnt on its load) before anything after this
 // statement, memory operations included
@@ -2496,15 +2553,15 @@ __device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s,
 template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
-    __shared__ T lut_s[kLutElems<T>];
+    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
-    const T* lut = lut_origin(lut_s + (lane % kLutCols<T>));
-    const int W = a.W, g = a.g, nS = a.nS, L = p.L, dec = t.dec, b = t.b;
-    T* const niw = a.nii_wr + ((size_t)dec * p.B + b) * nS * 16;
-    const T* const nir = a.nii_rd + ((size_t)dec * p.B + b) * nS * 16;
+    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, dec = t.dec, cwv = t.cwv;
+    T* const niw = a.nii_wr + ((size_t)dec * a.Bp + t.b) * nS * 16;
+    const T* const nir = a.nii_rd + ((size_t)dec * a.Bp + t.b) * nS * 16;
     const bool use_nii = a.nii && a.it > 0;
     const int base0 = t.s0 * W;
 
@@ -2546,7 +2603,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
     int bp = base0 + floor_div(ps - base0, S) * S;
     SwRaw<T> nx[S];
 #pragma unroll
-    for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, bp + m);
+    for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, lane, bp + m);
     for (; bp <= stop; bp += S) {
         // the segment's inputs from the prefetch registers, then the next segment's loads into them
         // (converting first keeps one copy of them live: no register moves at the loop edge)
@@ -2554,7 +2611,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
 #pragma unroll
         for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
 #pragma unroll
-        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, bp + S + m);
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, lane, bp + S + m);
         // Fast segments (all but about one in eight): whole, no chain start or NII position inside, each
         // chain stepping at every position or at none -- one straight block, the two chains' max*
         // interleaved.  The others take the per-position path below.
@@ -2656,22 +2713,30 @@ template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
                                                       const int* __restrict__ pinv)
 {
-    __shared__ T lut_s[kLutElems<T>];
+    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
     __shared__ alignas(16) T ck_lds[4 * 8 * 64];   // per wave: the next segment's checkpoint (DMA slot)
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
-    const T* lut = lut_origin(lut_s + (lane % kLutCols<T>));
-    const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, b = t.b;
-    T* const niw = a.nii_wr + ((size_t)dec * p.B + b) * nS * 16;
-    const T* const nir = a.nii_rd + ((size_t)dec * p.B + b) * nS * 16;
+    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, cwv = t.cwv, b = t.b;
+    T* const niw = a.nii_wr + ((size_t)dec * a.Bp + b) * nS * 16;
+    const T* const nir = a.nii_rd + ((size_t)dec * a.Bp + b) * nS * 16;
     const bool use_nii = a.nii && a.it > 0;
     const int base0 = t.s0 * W;
     const int* const perm = dec ? pi : pinv;
-    T* const le = a.le[dec] + (size_t)(b >> 6) * K * kSwCw + (b & 63);
+    T* const le = a.le[dec] + (size_t)cwv * K * kSwCw;
     uint8_t* const bitsT = dec ? a.bitsT : nullptr;
     const int bcol = t.cwv * 64 + lane;
+    // clock sample (as turbo_decode_kernel's): workgroup 0's shader clock and 100 MHz counter at its
+    // start and end, two scalar reads each, written by its first lane with one vector store
+    const bool clk = a.clk && p.clk && blockIdx.x == 0;
+    unsigned long long clk_c0 = 0, clk_r0 = 0;
+    if (clk) {
+        clk_c0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+    }
 
     int s = t.s1 - 1, st = 0, en = 0, qb = 0;
     bool hasB = false;
@@ -2722,7 +2787,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             for (int q = 0; q < kDma; ++q) dma16(ckslot_lds + q * 1024, src + q * 1024);
         }
 #pragma unroll
-        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, b, nbp + m);
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, lane, nbp + m);
     };
     prefetch(bp);
     // one position's LLR, extrinsic and decision (beta = beta[pos + 1]); `live`: the generic path's
@@ -2733,7 +2798,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
         const T lev = (llr - xm.la - (T)2 * xm.ys) * a.ext_scale;
         if (live) {
             if (pos < K) {
-                le[(size_t)perm[pos] * kSwCw] = lev;
+                le[(size_t)perm[pos] * kSwCw + lane] = lev;
                 if (bitsT) bitsT[(size_t)pi[pos] * a.Bp + bcol] = llr < (T)0 ? 0 : 1;
             }
             if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
@@ -2858,6 +2923,10 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
 #pragma unroll
                 for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
         }
+    }
+    if (clk) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) *reinterpret_cast<ulonglong4*>(p.clk) = make_ulonglong4(clk_c0, clk_r0, c1, r1);
     }
 }
 
@@ -2998,7 +3067,7 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.nii = w.nii;
     a.ckpt[0] = wb.ckpt[0];
     a.ckpt[1] = wb.ckpt[1];
-    const size_t nii_half = (size_t)2 * p.B * nS * 16;
+    const size_t nii_half = (size_t)2 * a.Bp * nS * 16;
     const int cw_total = a.Bp / 64;
     const bool split = ws.st2 && !p.all_iters && cw_total >= 2 * kSwHalfWaves;
     const int nparts = split ? 2 : 1;
@@ -3041,6 +3110,7 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 const Part& q = part[h];
                 a.cw0 = q.cw0;
                 a.ncw = q.ncw;
+                a.clk = h == 0 && it == p.iters - 1 && dec == (w.concurrent ? 0 : 1);   // one writer per decode
                 a.M = q.M;
                 a.nR = q.nR;
                 if (h == 1 && !forked) {   // half B starts one alpha launch behind half A

@@ -171,8 +171,9 @@ class TurboCodec:
         return a.value, b.value, n.value
 
     def clock(self):
-        """(sustained shader clock GHz, workgroup span ms) of the last exact-schedule turbo launch
-        (td_clock_read; synchronises the device)."""
+        """(sustained shader clock GHz, workgroup span ms) of the last decode: the exact schedule's
+        turbo launch, or a windowed decode's last SISO2 beta workgroup (td_clock_read; waits for
+        this handle's last decode)."""
         g, s = C.c_double(), C.c_double()
         N.check(N.lib().td_clock_read(self._h, C.byref(g), C.byref(s)))
         return g.value, s.value
