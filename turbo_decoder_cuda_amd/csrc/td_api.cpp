@@ -169,6 +169,11 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     dp.cu_slots = h->d_slots;
 }
 
+// The windowed beta kernel reads each wide array in whole segments of S rows by DMA (td_kernels.hip,
+// sw_beta_kernel), up to S - 1 rows past the last step of the last 64-codeword group: every wide array
+// carries that much slack (S x 64 x 8 bytes at most).
+constexpr size_t kWideSlack = 4096;
+
 // Workspace carve for G groups of the handle's K.  The alpha scratch (astore) belongs to the exact
 // schedule only, the tempmax stream (tmstore) to its Max-Log-MAP form only (log-MAP forms tempmax on
 // chip since round 4); the windowed schedule uses neither (its buffers: win_carve).  An absent region
@@ -182,8 +187,9 @@ Carve carve(int G, int K, size_t elem, int algo, bool exact)
     const int L = K + td::kMemory;
     // codewords: groups of 8 (exact schedule) or the windowed schedule's wide groups of 64
     const size_t ncw = exact ? (size_t)G * 8 : ((size_t)G * 8 + 63) / 64 * 64;
-    const size_t arrL = align_up(ncw * L * elem, 256);
-    const size_t arrK = align_up(ncw * K * elem, 256);
+    const size_t slack = exact ? 0 : kWideSlack;
+    const size_t arrL = align_up(ncw * L * elem + slack, 256);
+    const size_t arrK = align_up(ncw * K * elem + slack, 256);
     const size_t arrA = exact ? align_up(td::astore_elems(G, L) * elem, 256) : 0;
     const size_t arrT = exact && algo == TD_ALGO_MAXLOG ? arrL : 0;
     Carve c{};
@@ -392,7 +398,7 @@ WinCarve win_carve(const td_handle* h, int B)
     const size_t elem = h->elem;
     const int K = h->p.K, L = K + td::kMemory, G = groups_for(B);
     WinCarve c{};
-    c.arrK = align_up(((size_t)B + 63) / 64 * 64 * K * elem, 256);   // wide groups of 64 codewords
+    c.arrK = align_up(((size_t)B + 63) / 64 * 64 * K * elem + kWideSlack, 256);   // wide groups of 64 codewords
     c.nii = (size_t)2 * 2 * (((size_t)B + 63) / 64 * 64) * td::window_subblocks(L, h->wp.window) * 16 * elem;
     c.arrC = align_up(td::window_ckpt_elems(B, L, h->wp.window, elem == 4) * elem, 256);
     c.nii = align_up(c.nii, 256);

@@ -2498,6 +2498,17 @@ __device__ __forceinline__ void sw_set(T (&v)[8], int slot0_only, T x0)
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (j == 0 || !slot0_only) ? x0 : (T)-kInfty;
 }
+// a chain's NII start metrics, waited for here: a load left pending past the (rare) branch that issues
+// it made the compiler wait vmcnt(0) at every later use of the chain -- the next segment's prefetch
+// included
+template <typename T>
+__device__ __forceinline__ void sw_load_nii(T (&v)[8], const T* src)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(v[j]));
+}
 
 // the lane's task: decoder, run [s0, s1), codeword b (dead lanes of a partial wave compute on the
 // last codeword and store nothing)
@@ -2571,8 +2582,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
     if (i0 <= 0)
         sw_set(al, 1, (T)0);
     else if (use_nii)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) al[j] = nir[(size_t)t.s0 * 16 + j];
+        sw_load_nii(al, nir + (size_t)t.s0 * 16);
     else
         sw_set(al, 0, (T)0);
     sw_set(bl, 0, (T)0);
@@ -2648,6 +2658,17 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
                 sw_normalise(bl);
             }
         } else {
+            // sub-block s+1's chain starts at qb: set once at the segment's start (the positions below qb
+            // leave it alone), as a branch, not per-position selects (see the beta kernel)
+            if (hasB && qb >= bp && qb < bp + S && qb >= ps && qb <= stop) {
+                asm volatile("" ::: "memory");
+                if (qb <= 0)
+                    sw_set(bl, 1, (T)0);
+                else if (use_nii)
+                    sw_load_nii(bl, nir + (size_t)(s + 1) * 16);
+                else
+                    sw_set(bl, 0, (T)0);
+            }
 #pragma unroll
             for (int m = 0; m < S; ++m) {
                 const int pos = bp + m;
@@ -2660,15 +2681,6 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
                 if (s < nS - 1 && pos == qb && t.live)
 #pragma unroll
                     for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
-                if (hasB && pos == qb) {                     // sub-block s+1's chain starts here
-                    if (qb <= 0)
-                        sw_set(bl, 1, (T)0);
-                    else if (use_nii)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
-                    else
-                        sw_set(bl, 0, (T)0);
-                }
                 const bool doA = pos < need, doB = hasB && pos >= qb;
                 if (doA && doB)
                     sw_alpha_step2<T, ALGO>(al, bl, x[m], lut);
@@ -2688,8 +2700,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
 #pragma unroll
                     for (int j = 0; j < 8; ++j) niw[(size_t)(s + 1) * 16 + j] = al[j];
                 if (use_nii)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) bl[j] = nir[(size_t)(s + 1) * 16 + j];
+                    sw_load_nii(bl, nir + (size_t)(s + 1) * 16);
                 else
                     sw_set(bl, 0, (T)0);
             }
@@ -2715,6 +2726,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
 {
     __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
     __shared__ alignas(16) T ck_lds[4 * 8 * 64];   // per wave: the next segment's checkpoint (DMA slot)
+    __shared__ alignas(16) T in_lds[4 * 3 * S * 64];   // per wave: the next segment's ys, yp, La rows (DMA slot)
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
@@ -2754,8 +2766,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     if (e >= L)
         sw_set(be, 1, (T)0);
     else if (use_nii)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) be[j] = nir[(size_t)s * 16 + 8 + j];
+        sw_load_nii(be, nir + (size_t)s * 16 + 8);
     else
         sw_set(be, 0, (T)0);
     sw_set(bb, 0, (T)0);
@@ -2764,53 +2775,101 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
         for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = j == 0 ? (T)0 : (T)-kInfty;
     const int pe = min(e, L) - 1;                 // first position stepped
 
-    // Segment prefetch, one segment ahead: the inputs into registers and, for a segment of a sub-block's
-    // own range, its checkpoint (8 x 64 lane-contiguous values) into this wave's LDS slot by DMA
-    // (global_load_lds_dwordx4: no VGPR holds it in flight; in registers, with the merge of the
-    // segments that have none, it cost 46 VGPRs).  The DMA is issued BEFORE the input loads: VMEM loads
-    // complete in order, so once the compiler's wait for the first input load is past (sw_wait_on),
-    // the checkpoint has landed.  The slot is rewritten only after its reads (lgkmcnt(0)).
+    // Segment prefetch, one segment ahead, all of it by DMA into this wave's LDS slots
+    // (global_load_lds_dwordx4, 1 KB a wave instruction): the segment's three input rows (ys, yp, La:
+    // S consecutive 64-codeword rows each, contiguous in the wide layout) and, for a segment of a
+    // sub-block's own range, its checkpoint (8 x 64 lane-contiguous values).  Nothing in flight sits in
+    // a VGPR: with the inputs loaded into registers the allocator copied a pending load into the
+    // loop-carried register right after issuing it, so the wave waited for the prefetch it had just
+    // issued (vmcnt) in every segment.  Rows past the array ends stay inside the workspace (td_api.cpp:
+    // kWideSlack); their values are never used (positions >= L are not stepped, La >= K is masked).
+    // Ordering: the extrinsic / decision stores of a segment are issued at the start of the next one,
+    // before its DMA, so one `s_waitcnt vmcnt(0)` at each segment start covers exactly this segment's
+    // DMA and the stores before it, all issued a segment earlier.
     auto seg_sub = [&](int sbp) {                 // sub-block whose chain covers segment sbp
         return sbp >= en ? s : min(t.s0 + (sbp - base0) / W, t.s1 - 1);
     };
-    T* const ckslot = ck_lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 8 * 64;
-    const unsigned ckslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(ckslot));   // DMA base (M0): wave-uniform
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    T* const ckslot = ck_lds + wave * 8 * 64;
+    T* const inslot = in_lds + wave * 3 * S * 64;
+    const unsigned ckslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(ckslot));   // DMA bases (M0): wave-uniform
+    const unsigned inslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(inslot));
+    constexpr int kRowBytes = kSwCw * (int)sizeof(T);
+    constexpr int kInDma = S * kRowBytes / 1024;                    // DMA instructions per input array
+    static_assert(S * kRowBytes % 1024 == 0, "whole 1 KB DMA chunks");
     int bp = base0 + floor_div(pe - base0, S) * S;
-    SwRaw<T> nx[S];
+    // the segment's interleaver entries (wave-uniform: scalar loads), one segment ahead
+    int npm[S], npk[S];
     auto prefetch = [&](int nbp) {
+#pragma unroll
+        for (int m = 0; m < S; ++m) {
+            const int q = min(nbp + m, K - 1);
+            npm[m] = perm[q];
+            npk[m] = pi[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // the slots' previous reads are done
         const int ns = seg_sub(nbp), nst = ns * W;
         if (nbp >= base0 && nbp < sw_end(ns, nS, W, L)) {
             const char* src = reinterpret_cast<const char*>(sw_ck(a, t, ns, (nbp - nst) / S) - lane) + lane * 16;
-            constexpr int kDma = 8 * 64 * (int)sizeof(T) / 1024;   // 1 KB per wave instruction
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // the slot's previous reads are done
+            constexpr int kDma = 8 * 64 * (int)sizeof(T) / 1024;
 #pragma unroll
             for (int q = 0; q < kDma; ++q) dma16(ckslot_lds + q * 1024, src + q * 1024);
         }
+        const size_t row = (size_t)cwv * L + nbp, rowk = (size_t)cwv * K + nbp;
+        const char* src0 = reinterpret_cast<const char*>((dec ? p.sys2 : p.sys1) + row * kSwCw) + lane * 16;
+        const char* src1 = reinterpret_cast<const char*>((dec ? p.par2 : p.par1) + row * kSwCw) + lane * 16;
+        const char* src2 = reinterpret_cast<const char*>(a.la[dec] + rowk * kSwCw) + lane * 16;
 #pragma unroll
-        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, lane, nbp + m);
+        for (int q = 0; q < kInDma; ++q) {
+            dma16(inslot_lds + q * 1024, src0 + q * 1024);
+            dma16(inslot_lds + S * kRowBytes + q * 1024, src1 + q * 1024);
+            dma16(inslot_lds + 2 * S * kRowBytes + q * 1024, src2 + q * 1024);
+        }
     };
     prefetch(bp);
-    // one position's LLR, extrinsic and decision (beta = beta[pos + 1]); `live`: the generic path's
-    // stores skip the padding lanes (the fast path lets them store: they decode codeword B-1 again
-    // and write its own values to its own addresses, or to their own unused bitsT columns)
-    auto llr_out = [&](int pos, const T (&al)[8], const SwIn<T>& xm, bool live) {
+    // the previous segment's extrinsics and decisions, stored at the start of the next one
+    T dlev[S];
+    int dbit[S], dpm[S], dpk[S];
+    bool dst[S];
+#pragma unroll
+    for (int m = 0; m < S; ++m) dst[m] = false;
+    auto flush = [&] {
+#pragma unroll
+        for (int m = 0; m < S; ++m)
+            if (dst[m] && t.live) {
+                le[(size_t)dpm[m] * kSwCw + lane] = dlev[m];
+                if (bitsT) bitsT[(size_t)dpk[m] * a.Bp + bcol] = (uint8_t)dbit[m];
+            }
+    };
+    int pm[S], pk[S];
+    // one position's LLR, extrinsic and decision (beta = beta[pos + 1]), kept for the flush
+    auto llr_out = [&](int pos, const T (&al)[8], const SwIn<T>& xm, int m) {
         const T llr = sw_llr<T, ALGO>(al, be, xm, lut);
         const T lev = (llr - xm.la - (T)2 * xm.ys) * a.ext_scale;
-        if (live) {
-            if (pos < K) {
-                le[(size_t)perm[pos] * kSwCw + lane] = lev;
-                if (bitsT) bitsT[(size_t)pi[pos] * a.Bp + bcol] = llr < (T)0 ? 0 : 1;
-            }
-            if (p.le_dump) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
-        }
+        dlev[m] = lev;
+        dbit[m] = llr < (T)0 ? 0 : 1;
+        dst[m] = pos < K;
+        if (p.le_dump && t.live) p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
     };
     for (; bp >= base0; bp -= S) {
         SwIn<T> x[S];
         T as[S][8];
         const bool main = bp < en;                        // the segment lies in sub-block s's own range
-        sw_wait_on(nx[0].ys);                             // this segment's inputs, and its checkpoint DMA, landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this segment's DMA (and the stores before it)
+        flush();
 #pragma unroll
-        for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
+        for (int m = 0; m < S; ++m) {
+            SwRaw<T> r;
+            r.ys = inslot[m * 64 + lane];
+            r.yp = inslot[(S + m) * 64 + lane];
+            r.la = inslot[(2 * S + m) * 64 + lane];
+            x[m] = sw_cvt(r, bp + m < a.la_len);
+            pm[m] = npm[m];
+            pk[m] = npk[m];
+            dst[m] = false;
+            dpm[m] = pm[m];
+            dpk[m] = pk[m];
+        }
         if (main)
 #pragma unroll
             for (int j = 0; j < 8; ++j) as[0][j] = ckslot[j * 64 + lane];
@@ -2824,95 +2883,42 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
                 sw_fence();
             }
         }
-        // Fast segments: whole, every position in sub-block s's range (below K) or every one past it,
-        // no chain start strictly inside and no NII position, s-1's chain stepping everywhere or nowhere
         const int nb = st + g;                            // NII beta position of s-1
-        const bool whole = bp + S - 1 <= pe;
-        const bool allMain = bp + S <= en && bp + S <= K, noMain = bp >= en;
-        const bool binit_top = hasB && qb - 1 == bp + S - 1;
-        const bool bin = hasB && qb - 1 >= bp && qb - 1 < bp + S - 1;
-        const bool nbin = s > 0 && nb >= bp && nb < bp + S;
-        const bool bAll = hasB && bp + S - 1 < qb, bNone = !hasB || bp >= qb;
-#ifndef TD_SW_BETA_FAST
-#define TD_SW_BETA_FAST 0   // straight-line fast segments in the beta kernel (286 VGPRs: measured slower)
-#endif
-        if (TD_SW_BETA_FAST && whole && (allMain || noMain) && !bin && !nbin && (bAll || bNone)) {
-            if (binit_top) {                              // sub-block s-1's chain starts at qb = bp + S
-                if (qb >= L)
-                    sw_set(bb, 1, (T)0);
-                else if (use_nii)
+        // Sub-block s-1's chain starts at qb (its first step at qb - 1).  Its metrics are set once at
+        // the segment's start: the positions above qb - 1 leave them alone, so this equals setting
+        // them at qb - 1.  A branch, not a select (the empty asm keeps the compiler from if-converting
+        // it into 16 v_cndmask + 16 v_mov at every position: 8 % of the kernel's VALU).
+        if (hasB && qb - 1 >= bp && qb - 1 < bp + S && qb - 1 <= pe) {
+            asm volatile("" ::: "memory");
+            if (qb >= L)
+                sw_set(bb, 1, (T)0);
+            else if (use_nii)
+                sw_load_nii(bb, nir + (size_t)(s - 1) * 16 + 8);
+            else
+                sw_set(bb, 0, (T)0);
+        }
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
-                else
-                    sw_set(bb, 0, (T)0);
+        for (int m = S - 1; m >= 0; --m) {
+            const int pos = bp + m;
+            if (pos > pe) continue;
+            if (main && pos < en) llr_out(pos, as[m], x[m], m);
+            const bool doB = hasB && pos < qb;
+            if (doB)
+                sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
+            else
+                sw_beta_step<T, ALGO>(be, x[m], lut);
+            if (m == 0) {                                 // beta[bp]: an aligned position
+                sw_normalise(be);
+                if (doB) sw_normalise(bb);
             }
-            if (allMain && bAll) {
+            if (s > 0 && pos == nb && t.live)
 #pragma unroll
-                for (int m = S - 1; m >= 0; --m) {
-                    llr_out(bp + m, as[m], x[m], true);
-                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
-                    sw_fence();
-                }
-                sw_normalise(be);
-                sw_normalise(bb);
-            } else if (allMain) {
-#pragma unroll
-                for (int m = S - 1; m >= 0; --m) {
-                    llr_out(bp + m, as[m], x[m], true);
-                    sw_beta_step<T, ALGO>(be, x[m], lut);
-                    sw_fence();
-                }
-                sw_normalise(be);
-            } else if (bAll) {
-#pragma unroll
-                for (int m = S - 1; m >= 0; --m) {
-                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
-                    sw_fence();
-                }
-                sw_normalise(be);
-                sw_normalise(bb);
-            } else {
-#pragma unroll
-                for (int m = S - 1; m >= 0; --m) {
-                    sw_beta_step<T, ALGO>(be, x[m], lut);
-                    sw_fence();
-                }
-                sw_normalise(be);
-            }
-        } else {
-#pragma unroll
-            for (int m = S - 1; m >= 0; --m) {
-                const int pos = bp + m;
-                if (pos > pe) continue;
-                if (main && pos < en) llr_out(pos, as[m], x[m], t.live);
-                if (hasB && pos == qb - 1) {              // sub-block s-1's chain starts at qb
-                    if (qb >= L)
-                        sw_set(bb, 1, (T)0);
-                    else if (use_nii)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
-                    else
-                        sw_set(bb, 0, (T)0);
-                }
-                const bool doB = hasB && pos < qb;
-                if (doB)
-                    sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
-                else
-                    sw_beta_step<T, ALGO>(be, x[m], lut);
-                if (m == 0) {                             // beta[bp]: an aligned position
-                    sw_normalise(be);
-                    if (doB) sw_normalise(bb);
-                }
-                if (s > 0 && pos == nb && t.live)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
-            }
+                for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
         }
         if (hasB && bp == st) {                           // hand over to sub-block s-1
             if (qb <= st) {                               // g = 0: its chain starts at its end
                 if (use_nii)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) bb[j] = nir[(size_t)(s - 1) * 16 + 8 + j];
+                    sw_load_nii(bb, nir + (size_t)(s - 1) * 16 + 8);
                 else
                     sw_set(bb, 0, (T)0);
             }
@@ -2924,6 +2930,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
                 for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
         }
     }
+    flush();
     if (clk) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x == 0) *reinterpret_cast<ulonglong4*>(p.clk) = make_ulonglong4(clk_c0, clk_r0, c1, r1);
