@@ -159,8 +159,16 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
                     "traffic_frac": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic_frac_measured_ceiling": round(tb / (decode_ms * 1e-3) / 1e9 / HBM_MEASURED_GBS, 4),
                     "valu_instr_per_decode": int(vi), "valu_issue_frac": round(vi / cap, 4),
+                    # the two resource floors of the decode at this clock: all VALU issue slots busy, or the
+                    # counter bytes at the measured streaming ceiling; the kernels overlap the two (two
+                    # streams), so the larger floor binds and frac_of_binding = floor / decode time
+                    "valu_floor_ms": round(vi * 4.0 / N_SIMDS / (clk * 1e9) * 1e3, 3),
+                    "hbm_floor_ms": round(tb / (HBM_MEASURED_GBS * 1e9) * 1e3, 3),
                     "sclk_ghz": round(clk, 4), "sclk_source": "measured (td_clock_read: one beta workgroup)" if sclk_ghz else "constant",
                     "pmc_source": rec.get("source"), "kernel": rec.get("kernel")})
+        floor = max(out["valu_floor_ms"], out["hbm_floor_ms"])
+        out.update({"binding": "valu" if out["valu_floor_ms"] >= out["hbm_floor_ms"] else "hbm",
+                    "frac_of_binding": round(floor / decode_ms, 4)})
     return out
 
 
