@@ -837,7 +837,7 @@ int td_set_window(td_handle* h, const td_window_params* w)
 {
     if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
     if (!w || w->window == 0) {
-        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0};
+        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0, 0};
         return TD_OK;
     }
     if (w->window < 3 || w->window > 10000) return fail(TD_EINVAL, "td_set_window: window must be 0 or in [3, 10000]");
@@ -848,8 +848,9 @@ int td_set_window(td_handle* h, const td_window_params* w)
     // TD_WINDOW_RUN (environment, tests): sub-blocks per lane run, forcing the run layout on batches too
     // small to choose it (the results do not depend on it)
     const char* run = std::getenv("TD_WINDOW_RUN");
+    const char* run_a = std::getenv("TD_WINDOW_RUN_A");
     h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale,
-                             run ? std::atoi(run) : 0};
+                             run ? std::atoi(run) : 0, run_a ? std::atoi(run_a) : 0};
     return TD_OK;
 }
 

@@ -102,6 +102,7 @@ struct WindowParams {
     int concurrent;    // both SISOs per launch on the previous iteration's extrinsics
     double ext_scale;  // extrinsic scaling (1 = none)
     int run;           // sub-blocks per lane run, 0 = chosen by window_run (TD_WINDOW_RUN, tests)
+    int run_a;         // the alpha kernel's, if non-zero (TD_WINDOW_RUN_A, measurements)
 };
 // extra device buffers of the windowed schedule
 template <typename T>

@@ -2553,6 +2553,10 @@ __device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s,
 }
 
 // ---- alpha: forward over the run, checkpoints every S positions of each sub-block
+// TD_SW_ALPHA_PRIO > 0: the alpha waves issue ahead of co-resident beta waves (s_setprio)
+#ifndef TD_SW_ALPHA_PRIO
+#define TD_SW_ALPHA_PRIO 0
+#endif
 #ifndef TD_SW_ALPHA_WAVES
 #define TD_SW_ALPHA_WAVES 0
 #endif
@@ -2565,6 +2569,7 @@ template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
+    if constexpr (TD_SW_ALPHA_PRIO > 0) __builtin_amdgcn_s_setprio(TD_SW_ALPHA_PRIO);
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
@@ -3028,9 +3033,14 @@ constexpr int sw_seg()
 
 // sub-blocks per lane run: one (M = 1) while a launch has fewer than kSwRunWaves one-sub-block waves,
 // else as many as keep about that many waves; runs need g <= W (two chains at most) and W a multiple
-// of S (every sub-block start is a segment start)
+// of S (every sub-block start is a segment start).  Each run's first chain starts g steps early on
+// its own (and its last ends g steps late), so fewer, longer runs do less work: at config 5 (96
+// sub-blocks, 512 waves of codewords) M = 24 leaves 4 runs a codeword, 2 % extra steps against M = 6's
+// 7.8 %, and 2048 waves a SISO -- one round of the beta kernel's 2048 slots (2 waves a SIMD) over the
+// two halves.  Measured (round 5, same box, TD_WINDOW_RUN): M = 6 2462, 8 2467, 12 2553, 20 2525
+// (1.25 rounds), 24 2628, 32 2236 (3/4 of the slots), 48 1559 Mbit/s.
 #ifndef TD_SW_RUN_WAVES
-#define TD_SW_RUN_WAVES 8192
+#define TD_SW_RUN_WAVES 2048
 #endif
 constexpr int kSwRunWaves = TD_SW_RUN_WAVES;
 
@@ -3079,16 +3089,19 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     const bool split = ws.st2 && !p.all_iters && cw_total >= 2 * kSwHalfWaves;
     const int nparts = split ? 2 : 1;
     struct Part {
-        int cw0, ncw, M, nR, blocks;
+        int cw0, ncw, M, nR, blocks, Ma, nRa, blocksa;
         hipStream_t s;
     } part[2];
     for (int h = 0; h < nparts; ++h) {
         Part& q = part[h];
         q.cw0 = h == 0 ? 0 : cw_total / 2;
         q.ncw = nparts == 1 ? cw_total : (h == 0 ? cw_total / 2 : cw_total - cw_total / 2);
-        q.M = window_run(p.L, W, w.overlap, q.ncw * 64, ndec, S, w.run);
+        q.M = window_run(p.L, W, w.overlap, cw_total * 64, ndec, S, w.run);   // sized on the whole batch (both halves co-run)
         q.nR = (nS + q.M - 1) / q.M;
         q.blocks = (int)(((long long)q.nR * q.ncw * ndec + 3) / 4);
+        q.Ma = w.run_a > 0 ? window_run(p.L, W, w.overlap, cw_total * 64, ndec, S, w.run_a) : q.M;
+        q.nRa = (nS + q.Ma - 1) / q.Ma;
+        q.blocksa = (int)(((long long)q.nRa * q.ncw * ndec + 3) / 4);
         q.s = h == 0 ? st : ws.st2;
     }
     auto check = [] { return hipGetLastError(); };
@@ -3118,14 +3131,16 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 a.cw0 = q.cw0;
                 a.ncw = q.ncw;
                 a.clk = h == 0 && it == p.iters - 1 && dec == (w.concurrent ? 0 : 1);   // one writer per decode
-                a.M = q.M;
-                a.nR = q.nR;
                 if (h == 1 && !forked) {   // half B starts one alpha launch behind half A
                     hipError_t e = hipStreamWaitEvent(q.s, ws.fork, 0);
                     if (e != hipSuccess) return e;
                     forked = true;
                 }
-                hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocks), dim3(256), 0, q.s, p, a);
+                a.M = q.Ma;
+                a.nR = q.nRa;
+                hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocksa), dim3(256), 0, q.s, p, a);
+                a.M = q.M;
+                a.nR = q.nR;
                 if (h == 0 && split && !forked) {
                     hipError_t e = hipEventRecord(ws.fork, q.s);
                     if (e != hipSuccess) return e;
