@@ -96,7 +96,7 @@ struct td_handle {
     td::WindowParams wp{0, 0, 0, 0, 1.0, 0};
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
-    td::WindowStreams wstr{nullptr, nullptr, nullptr};   // the windowed schedule's second stream (halves)
+    td::WindowStreams wstr{};                    // the windowed schedule's extra streams (batch parts)
     // Workspace ordering across streams: every decode uses the same d_ws / d_wws, so a decode
     // issued on a stream other than the previous decode's first waits (on the device) for that
     // decode to finish with the workspace.  Decodes on one handle therefore never overlap; callers
@@ -511,10 +511,12 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
     if (h->wp.window) {
-        if (!h->wstr.st2) {   // created once, on the handle's device (the decode's caller stream is the first)
-            TD_HIP(hipStreamCreateWithFlags(&h->wstr.st2, hipStreamNonBlocking));
-            TD_HIP(hipEventCreateWithFlags(&h->wstr.fork, hipEventDisableTiming));
-            TD_HIP(hipEventCreateWithFlags(&h->wstr.join, hipEventDisableTiming));
+        if (!h->wstr.st[1]) {   // created once, on the handle's device (part 0 runs on the caller's stream)
+            for (int i = 1; i < td::kSwMaxParts; ++i) {
+                TD_HIP(hipStreamCreateWithFlags(&h->wstr.st[i], hipStreamNonBlocking));
+                TD_HIP(hipEventCreateWithFlags(&h->wstr.fork[i], hipEventDisableTiming));
+                TD_HIP(hipEventCreateWithFlags(&h->wstr.join[i], hipEventDisableTiming));
+            }
         }
         e = td::launch_window<T>(dp, h->wp, wb, st, h->wstr);
     }
@@ -804,9 +806,11 @@ int td_destroy(td_handle* h)
     if (h->d_hle) (void)hipFree(h->d_hle);
     if (h->d_win) (void)hipFree(h->d_win);
     if (h->d_wws) (void)hipFree(h->d_wws);
-    if (h->wstr.st2) (void)hipStreamDestroy(h->wstr.st2);
-    if (h->wstr.fork) (void)hipEventDestroy(h->wstr.fork);
-    if (h->wstr.join) (void)hipEventDestroy(h->wstr.join);
+    for (int i = 1; i < td::kSwMaxParts; ++i) {
+        if (h->wstr.st[i]) (void)hipStreamDestroy(h->wstr.st[i]);
+        if (h->wstr.fork[i]) (void)hipEventDestroy(h->wstr.fork[i]);
+        if (h->wstr.join[i]) (void)hipEventDestroy(h->wstr.join[i]);
+    }
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     if (h->ws_free) (void)hipEventDestroy(h->ws_free);
@@ -837,7 +841,7 @@ int td_set_window(td_handle* h, const td_window_params* w)
 {
     if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
     if (!w || w->window == 0) {
-        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0, 0};
+        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0, 0, 0};
         return TD_OK;
     }
     if (w->window < 3 || w->window > 10000) return fail(TD_EINVAL, "td_set_window: window must be 0 or in [3, 10000]");
@@ -849,8 +853,9 @@ int td_set_window(td_handle* h, const td_window_params* w)
     // small to choose it (the results do not depend on it)
     const char* run = std::getenv("TD_WINDOW_RUN");
     const char* run_a = std::getenv("TD_WINDOW_RUN_A");
+    const char* parts = std::getenv("TD_WINDOW_PARTS");
     h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale,
-                             run ? std::atoi(run) : 0, run_a ? std::atoi(run_a) : 0};
+                             run ? std::atoi(run) : 0, run_a ? std::atoi(run_a) : 0, parts ? std::atoi(parts) : 0};
     return TD_OK;
 }
 

@@ -103,6 +103,7 @@ struct WindowParams {
     double ext_scale;  // extrinsic scaling (1 = none)
     int run;           // sub-blocks per lane run, 0 = chosen by window_run (TD_WINDOW_RUN, tests)
     int run_a;         // the alpha kernel's, if non-zero (TD_WINDOW_RUN_A, measurements)
+    int parts;         // batch parts on as many streams, 0 = 2 (TD_WINDOW_PARTS, measurements)
 };
 // extra device buffers of the windowed schedule
 template <typename T>
@@ -121,9 +122,11 @@ size_t window_bits_bytes(int B, int K);
 // that many where runs are possible (g <= W, W a multiple of the checkpoint spacing S)
 int window_run(int L, int W, int g, int B, int ndec, int S, int force = 0);
 // the handle's second stream and its fork / join events (timing disabled); st2 null: one stream
+// the windowed schedule's batch parts run on the caller's stream (part 0) and st[1..] (launch_window_algo)
+constexpr int kSwMaxParts = 4;
 struct WindowStreams {
-    hipStream_t st2;
-    hipEvent_t fork, join;
+    hipStream_t st[kSwMaxParts];   // st[0] unused
+    hipEvent_t fork[kSwMaxParts], join[kSwMaxParts];
 };
 template <typename T>
 hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st,

@@ -3086,26 +3086,28 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.ckpt[1] = wb.ckpt[1];
     const size_t nii_half = (size_t)2 * a.Bp * nS * 16;
     const int cw_total = a.Bp / 64;
-    const bool split = ws.st2 && !p.all_iters && cw_total >= 2 * kSwHalfWaves;
-    const int nparts = split ? 2 : 1;
+    // batch parts: 2 by default (TD_WINDOW_PARTS: measured 3 and 4 slower, profiles/r05/sweep_window_layout.txt)
+    const int want = w.parts > 0 ? min(w.parts, kSwMaxParts) : 2;
+    const int nparts = (ws.st[1] && !p.all_iters) ? max(1, min(want, cw_total / kSwHalfWaves)) : 1;
+    const bool split = nparts > 1;
     struct Part {
         int cw0, ncw, M, nR, blocks, Ma, nRa, blocksa;
         hipStream_t s;
-    } part[2];
+    } part[kSwMaxParts];
     for (int h = 0; h < nparts; ++h) {
         Part& q = part[h];
-        q.cw0 = h == 0 ? 0 : cw_total / 2;
-        q.ncw = nparts == 1 ? cw_total : (h == 0 ? cw_total / 2 : cw_total - cw_total / 2);
+        q.cw0 = (int)((long long)cw_total * h / nparts);
+        q.ncw = (int)((long long)cw_total * (h + 1) / nparts) - q.cw0;
         q.M = window_run(p.L, W, w.overlap, cw_total * 64, ndec, S, w.run);   // sized on the whole batch (both halves co-run)
         q.nR = (nS + q.M - 1) / q.M;
         q.blocks = (int)(((long long)q.nR * q.ncw * ndec + 3) / 4);
         q.Ma = w.run_a > 0 ? window_run(p.L, W, w.overlap, cw_total * 64, ndec, S, w.run_a) : q.M;
         q.nRa = (nS + q.Ma - 1) / q.Ma;
         q.blocksa = (int)(((long long)q.nRa * q.ncw * ndec + 3) / 4);
-        q.s = h == 0 ? st : ws.st2;
+        q.s = h == 0 ? st : ws.st[h];
     }
     auto check = [] { return hipGetLastError(); };
-    bool forked = false;
+    bool forked[kSwMaxParts] = {}, recorded[kSwMaxParts] = {};
     for (int it = 0; it < p.iters; ++it) {
         a.it = it;
         a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
@@ -3131,19 +3133,20 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 a.cw0 = q.cw0;
                 a.ncw = q.ncw;
                 a.clk = h == 0 && it == p.iters - 1 && dec == (w.concurrent ? 0 : 1);   // one writer per decode
-                if (h == 1 && !forked) {   // half B starts one alpha launch behind half A
-                    hipError_t e = hipStreamWaitEvent(q.s, ws.fork, 0);
+                if (h > 0 && !forked[h]) {   // part h starts one alpha launch behind part h-1
+                    hipError_t e = hipStreamWaitEvent(q.s, ws.fork[h], 0);
                     if (e != hipSuccess) return e;
-                    forked = true;
+                    forked[h] = true;
                 }
                 a.M = q.Ma;
                 a.nR = q.nRa;
                 hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocksa), dim3(256), 0, q.s, p, a);
                 a.M = q.M;
                 a.nR = q.nR;
-                if (h == 0 && split && !forked) {
-                    hipError_t e = hipEventRecord(ws.fork, q.s);
+                if (h + 1 < nparts && !recorded[h + 1]) {
+                    hipError_t e = hipEventRecord(ws.fork[h + 1], q.s);
                     if (e != hipSuccess) return e;
+                    recorded[h + 1] = true;
                 }
                 hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S>), dim3(q.blocks), dim3(256), 0, q.s, p, a, p.pi, p.pinv);
                 hipError_t e = check();
@@ -3158,10 +3161,13 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
             if (e != hipSuccess) return e;
         }
     }
-    if (split) {   // join half B back into the caller's stream, then the decisions
-        hipError_t e = hipEventRecord(ws.join, ws.st2);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, ws.join, 0);
-        if (e != hipSuccess) return e;
+    if (split) {   // join the other parts back into the caller's stream, then the decisions
+        for (int h = 1; h < nparts; ++h) {
+            hipError_t e = hipEventRecord(ws.join[h], ws.st[h]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, ws.join[h], 0);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e;
         hipLaunchKernelGGL(bits_transpose_kernel, dim3((p.K + 63) / 64, a.Bp / 64), dim3(256), 0, st, wb.bitsT, p.K,
                            a.Bp, p.B, p.bits, (long long)p.K);
         e = check();
