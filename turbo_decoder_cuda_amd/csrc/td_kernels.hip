@@ -317,11 +317,9 @@ static_assert(kFoldA <= kLanes && kTile - kFoldA <= kLanes, "one fold item per l
 // fp64 Max-Log-MAP, whose B pass the two fold waves (A and F0) bound: A takes 64 items (8 whole
 // steps), F0 the other 56 (profiles/r04/ab_v32_maxlog_foldsplit.txt: config 3 +1.2 %, its 32768
 // batch +1.5 %; 56/64 the same; fp32 Max-Log-MAP lost 1.5 % either way and keeps 60/60).
-#ifndef TD_FOLDA_MAX
-#define TD_FOLDA_MAX 64
-#endif
+constexpr int kFoldAMaxLog64 = 64;
 template <typename T, int ALGO>
-constexpr int kFoldAOf = (ALGO == 1 && sizeof(T) == 8) ? TD_FOLDA_MAX : kFoldA;   // items of fold wave A
+constexpr int kFoldAOf = (ALGO == 1 && sizeof(T) == 8) ? kFoldAMaxLog64 : kFoldA;   // items of fold wave A
 static_assert(kFoldAOf<double, 1> <= kLanes && kTile - kFoldAOf<double, 1> <= kLanes, "one fold item per lane");
 constexpr int kAvSlots = 4;   // alpha ring: copied 3 iterations before its fold (loader depth 3)
 // every alpha row of a window is in the Av ring for the folds (no fold-side recompute)
@@ -1553,18 +1551,10 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 // (beta bounds its B pass; F1 measured 0.5 % slower, fp32 0.8 %); Max-Log-MAP, whose B pass the
 // folds and the loader bound, moves it to F1 (+3.0 %, config 3).  The F pass then stages nothing
 // past the last window (kFSkip), so no F-pass DMA is in flight when F1 starts staging.
-#ifndef TD_BLOADER_LOG
-#define TD_BLOADER_LOG 2
-#endif
-#ifndef TD_BLOADER_MAX
-#define TD_BLOADER_MAX 3
-#endif
 template <int ALGO>
-constexpr int kBLoaderWave = ALGO == 1 ? TD_BLOADER_MAX : TD_BLOADER_LOG;
+constexpr int kBLoaderWave = ALGO == 1 ? 3 : 2;
 template <int ALGO>
 constexpr bool kFSkip = kBLoaderWave<ALGO> == 3;   // (on its own, with F0 loading both passes: level)
-static_assert(TD_BLOADER_LOG == 2 || TD_BLOADER_LOG == 3, "B-pass loader: wave 2 or 3");
-static_assert(TD_BLOADER_MAX == 2 || TD_BLOADER_MAX == 3, "B-pass loader: wave 2 or 3");
 constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
 // The lane index made opaque at the start of every SISO (role remat), so that the compiler cannot
 // hoist the roles' lane-derived addresses (fold lanes, alpha store offsets, ...) out of the SISO loop,
@@ -2553,10 +2543,7 @@ __device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s,
 }
 
 // ---- alpha: forward over the run, checkpoints every S positions of each sub-block
-// TD_SW_ALPHA_PRIO > 0: the alpha waves issue ahead of co-resident beta waves (s_setprio)
-#ifndef TD_SW_ALPHA_PRIO
-#define TD_SW_ALPHA_PRIO 0
-#endif
+// (s_setprio 2 on the alpha waves, to issue ahead of a co-resident beta wave, measured level: not kept)
 #ifndef TD_SW_ALPHA_WAVES
 #define TD_SW_ALPHA_WAVES 0
 #endif
@@ -2569,7 +2556,6 @@ template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
-    if constexpr (TD_SW_ALPHA_PRIO > 0) __builtin_amdgcn_s_setprio(TD_SW_ALPHA_PRIO);
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
