@@ -112,3 +112,37 @@ def test_launch_clock_and_host_staging_reuse():
             for b, fr in enumerate(range(5)[rows]):
                 ob, _ = O.turbo_decode(flow[fr], K, f1, f2, iters)
                 assert np.array_equal(out[b].astype(np.uint8), ob.astype(np.uint8)), (rows, fr)
+
+
+def test_graph_capture_windowed_two_streams():
+    """A windowed decode large enough to run in two batch parts (two streams, fork / join events)
+    captured into a hipGraph: both replays equal the eager decode of the same input bit for bit, and
+    sampled codewords of both parts equal the C restatement of the windowed schedule."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    K, f1, f2, iters, W, g = 512, 31, 64, 3, 64, 30
+    B = 2 * 64 * 64 + 5                      # 129 waves of 64 codewords: two parts
+    dev = _dev()
+    flows = [np.tile(O.synth_batch(K, f1, f2, 0.3 + 0.2 * k, 900 + k, 64)[1], (B // 64 + 1, 1))[:B] for k in range(2)]
+    xs = [torch.from_numpy(np.ascontiguousarray(f)).to(dev) for f in flows]
+    sb = torch.cuda.Stream(dev)
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.set_window(W, g)
+        c.reserve(B)
+        eager = [c.decode(x).cpu().numpy() for x in xs]   # (the first windowed decode creates the streams)
+        torch.cuda.synchronize()
+        gin = xs[0].clone()
+        gout = torch.empty((B, K), dtype=torch.uint8, device=dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=sb):
+            c.decode(gin, gout, stream=sb)
+        for k in (0, 1):
+            gin.copy_(xs[k])
+            graph.replay()
+            torch.cuda.synchronize()
+            assert np.array_equal(gout.cpu().numpy(), eager[k]), k
+    for k in (0, 1):
+        for b in (3, 64 * 64 + 9, B - 1):
+            ob, _ = O.turbo_decode_window(flows[k][b], K, f1, f2, iters, W, g)
+            assert np.array_equal(eager[k][b], ob[-1]), (k, b)
