@@ -2250,11 +2250,15 @@ __global__ __launch_bounds__(kWaves * 64, 2) void siso_kernel(DecodeParams<T> p,
 //   sw_beta_kernel   beta backward over the run in segments of S positions: the segment's alpha
 //                    recomputed from its checkpoint into registers, then beta and the LLR fold;
 //                    over the first g positions of sub-block s, s-1's beta warm-up chain runs beside.
-// Both prefetch the next segment's inputs (and checkpoint) one segment ahead.  SISO2's decisions go
-// to a [K][Bp] byte array (a wave's 64 codewords adjacent) that bits_transpose_kernel turns into
-// [B][K]: written directly, each byte of a wave store landed on its own cache line.
-// Round 4's single kernel (one sub-block per lane, loads waited at each segment start, the
-// interleaver index loaded and waited before every extrinsic store) ran config 5 at 2306-2328 Mbit/s.
+// Both prefetch the next segment's inputs (and checkpoint) one segment ahead: alpha into registers,
+// beta by LDS DMA with its extrinsic / decision stores deferred to the next segment's start.  SISO2's
+// decisions go to a [K][Bp] byte array (a wave's 64 codewords adjacent) that bits_transpose_kernel
+// turns into [B][K]: written directly, each byte of a wave store landed on its own cache line.
+// launch_window_algo runs the batch in two parts on two streams, so one part's alpha (HBM-heavy)
+// co-runs with the other's beta (VALU-heavy), and sizes the lane runs so that one beta round covers
+// both parts.  Round 4's single kernel (one sub-block per lane, loads waited at each segment start,
+// the interleaver index loaded and waited before every extrinsic store) ran config 5 at 2306-2328
+// Mbit/s; these kernels run it at about 2620.
 template <typename T>
 struct WinArgs {
     int W, g;              // sub-block length, overlap
@@ -2268,7 +2272,7 @@ struct WinArgs {
     int it;                // iteration
     int la_len;            // La valid for steps < la_len (0 before any extrinsic exists)
     int nii;               // boundary metrics from nii_rd (after the first iteration)
-    const T* la[2];        // per decoder: La [G][K][8] (dec 0 natural order, dec 1 interleaved)
+    const T* la[2];        // per decoder: La, wide [B/64][K][64] (dec 0 natural order, dec 1 interleaved)
     T* le[2];              // per decoder: Le out, scattered to the other decoder's order
     const T* nii_rd;       // [2 dec][B][nS][2][8]: alpha (0) / beta (1) at the chain's start
     T* nii_wr;
