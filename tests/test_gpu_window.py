@@ -122,7 +122,11 @@ def test_window_f32_vs_c_restatement(monkeypatch, algo, run):
         assert np.abs(le[b] - ol).max() <= 1e-4 * max(1.0, np.abs(ol).max()), f"codeword {b}"
 
 
-def test_window_batch_parts_and_runs_do_not_change_results(monkeypatch):
+@pytest.mark.parametrize("nii,conc,scale,precision,algo", [(False, False, 1.0, "f64", "logmap"),
+                                                         (True, True, 0.77, "f64", "logmap"),
+                                                         (False, False, 1.0, "f32", "logmap"),
+                                                         (True, True, 0.77, "f32", "maxlog")])
+def test_window_batch_parts_and_runs_do_not_change_results(monkeypatch, nii, conc, scale, precision, algo):
     """Large batches run in parts on several streams (one part's alpha beside another's beta), with
     lane runs sized on the whole batch and the alpha kernel's own run length: none of it may change a
     bit.  A ragged batch big enough for four parts, decoded with 1, 2, 3 and 4 parts and two alpha
@@ -135,15 +139,18 @@ def test_window_batch_parts_and_runs_do_not_change_results(monkeypatch):
     B = 4 * 64 * 64 + 37                      # 257 waves of 64 codewords
     _, flow = O.synth_batch(K, f1, f2, 0.4, 5, 64)
     flow = np.tile(flow, (B // 64 + 1, 1))[:B]
-    x = torch.from_numpy(flow).to("cuda:0")
+    if precision == "f32":
+        flow = flow.astype(np.float32)
+    dt = torch.float64 if precision == "f64" else torch.float32
+    x = torch.from_numpy(np.ascontiguousarray(flow)).to("cuda:0")
     outs = {}
     for parts, run_a in ((1, 0), (2, 0), (3, 0), (4, 0), (2, 1), (4, 3)):
         monkeypatch.setenv("TD_WINDOW_PARTS", str(parts))
         monkeypatch.setenv("TD_WINDOW_RUN_A", str(run_a))
-        with TurboCodec(K, f1, f2, iterations=iters) as c:
-            c.set_window(W, g)
+        with TurboCodec(K, f1, f2, iterations=iters, algo=algo, precision=precision) as c:
+            c.set_window(W, g, scale, nii=nii, concurrent=conc)
             bits = torch.empty((B, K), dtype=torch.uint8, device=x.device)
-            le = torch.empty((B, iters, 2, K + 3), dtype=torch.float64, device=x.device)
+            le = torch.empty((B, iters, 2, K + 3), dtype=dt, device=x.device)
             c.decode(x, bits, le=le)
             torch.cuda.synchronize()
         outs[(parts, run_a)] = (bits.cpu().numpy(), le.cpu().numpy())
@@ -151,10 +158,13 @@ def test_window_batch_parts_and_runs_do_not_change_results(monkeypatch):
     for key, (bk, lk) in outs.items():
         assert np.array_equal(bk, b1), key
         assert np.array_equal(lk, l1), key
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
     for b in (0, 64 * 64 + 5, 2 * 64 * 64 + 11, B - 1):   # one codeword in each of the four parts
-        ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g)
+        ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo, nii=nii, concurrent=conc,
+                                       scale=scale)
         assert np.array_equal(b1[b], ob[-1]), b
-        assert np.abs(l1[b] - ol).max() <= 1e-9, b
+        tol = 1e-9 if precision == "f64" else 1e-4 * max(1.0, np.abs(ol).max())
+        assert np.abs(l1[b] - ol).max() <= tol, b
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
