@@ -48,6 +48,10 @@ FRAME_CASES = [
     (72, 7, 18, 0.5, 44, 3, 4, np.float64),
     (88, 5, 22, 0.5, 45, 3, 4, np.float64),
     (432, 47, 72, 0.8, 46, 2, 4, np.float64),
+    # round 5: more K = 6144 frames (the benchmark size had two frames of one seed): two seeds, two
+    # frames each, below and above the waterfall
+    (6144, 263, 480, 0.0, 22, 2, 8, np.float32),
+    (6144, 263, 480, 0.6, 23, 2, 8, np.float32),
 ]
 
 
@@ -100,12 +104,18 @@ def gen_maxstar(n, seed):
 
 
 def main():
+    """All fixtures; with arguments `frames K:seed ...`, only those frame fixtures (the others keep
+    their bytes)."""
     if not os.path.exists(HARNESS):
         subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
     os.makedirs(GOLD, exist_ok=True)
-    made = [gen_maxstar(2000, 7), gen_siso(1027, 1, 5), gen_siso(1027, 0, 6), gen_siso(43, 1, 8)]
-    for case in FRAME_CASES:
-        made.append(gen_frames(*case))
+    if len(sys.argv) > 2 and sys.argv[1] == "frames":
+        want = {tuple(int(v) for v in a.split(":")) for a in sys.argv[2:]}
+        made = [gen_frames(*c) for c in FRAME_CASES if (c[0], c[4]) in want]
+    else:
+        made = [gen_maxstar(2000, 7), gen_siso(1027, 1, 5), gen_siso(1027, 0, 6), gen_siso(43, 1, 8)]
+        for case in FRAME_CASES:
+            made.append(gen_frames(*case))
     for m in made:
         print(m, os.path.getsize(os.path.join(GOLD, m)))
 
