@@ -100,3 +100,24 @@ def test_power_sampler_is_inert_without_a_gpu():
     import bench
     s = bench.PowerSampler(0).start()
     assert s.stop() is None
+
+
+def test_window_roofline_record():
+    """bench.window_roofline (config 5's roofline object) from the committed PMC record: both floors
+    present and consistent with the record (VALU: 4 cycles per wave64 instruction on 1024 SIMDs at the
+    given clock; HBM: counter bytes at the measured ceiling), the binding one named, and the fraction
+    = the binding floor / the decode time."""
+    import json
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+
+    rec = json.load(open(os.path.join(REPO, "profiles", "traffic.json")))["K6144_B32768_it8_f64_logmap_w64g30"]
+    r = bench.window_roofline(6144, 32768, 8, 80.0, 2.2)
+    assert r["traffic"] == rec["bytes_per_decode"] and r["valu_instr_per_decode"] == rec["valu_instr_per_decode"]
+    assert abs(r["valu_floor_ms"] - rec["valu_instr_per_decode"] * 4 / 1024 / 2.2e9 * 1e3) < 1e-2
+    assert abs(r["hbm_floor_ms"] - rec["bytes_per_decode"] / (bench.HBM_MEASURED_GBS * 1e9) * 1e3) < 1e-2
+    floor = max(r["valu_floor_ms"], r["hbm_floor_ms"])
+    assert r["binding"] == ("valu" if r["valu_floor_ms"] >= r["hbm_floor_ms"] else "hbm")
+    assert abs(r["frac_of_binding"] - floor / 80.0) < 1e-3
+    assert 0 < r["valu_issue_frac"] < 1 and 0 < r["traffic_frac"] < 1
