@@ -6,13 +6,12 @@
 set -e
 cd "$(dirname "$0")/.."
 PKG=turbo_decoder_cuda_amd
-rm -f $PKG/libvar_*.so
+rm -rf $PKG/libvar_*.so $PKG/libvar_*.so.objs
 for v in $VARIANTS; do
   name=${v%%:*}
   flags=${v#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-honor-nans \
-    -Iinclude -I$PKG/csrc ${flags//,/ } -shared -o $PKG/libvar_$name.so \
-    $PKG/csrc/td_kernels.hip $PKG/csrc/td_kernels_w12.hip $PKG/csrc/td_synth.hip $PKG/csrc/td_api.cpp &
+  python -c "import sys; from turbo_decoder_cuda_amd import build; build.build_lib(sys.argv[1], sys.argv[2:])" \
+    $PKG/libvar_$name.so ${flags//,/ } > /dev/null &
 done
 wait
 ls -la $PKG/libvar_*.so

@@ -32,7 +32,8 @@ def test_host_abi_under_asan_ubsan(tmp_path):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-ffp-contract=off",
            "-fno-honor-nans", f"-I{REPO}/include", f"-I{CSRC}", *hip_san,
            os.path.join(REPO, "tests", "host_abi_sanitize.cpp"), os.path.join(CSRC, "td_api.cpp"),
-           os.path.join(CSRC, "td_kernels.hip"), os.path.join(CSRC, "td_kernels_w12.hip"), os.path.join(CSRC, "td_synth.hip"), "-o", exe]
+           os.path.join(CSRC, "td_kernels.hip"), os.path.join(CSRC, "td_kernels_w12.hip"), os.path.join(CSRC, "td_kernels_win.hip"),
+           os.path.join(CSRC, "td_synth.hip"), "-o", exe]
     subprocess.check_call(cmd)
     r = _run(exe)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]

@@ -68,26 +68,62 @@ def _workers(n: int) -> int:
     return max(1, min(n, int(avail // 6)))
 
 
+# td_kernels_win.hip (the sub-block schedule) under the max-ILP machine scheduler: +1.4 % at BASELINE
+# config 5; the exact kernels (td_kernels.hip) lose 1 % under it and keep the default.
+WIN_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+SRCS = ("td_kernels.hip", "td_kernels_w12.hip", "td_kernels_win.hip", "td_synth.hip", "td_api.cpp")
+FILE_FLAGS = {"td_kernels_win.hip": WIN_FLAGS}
+
+
+def lib_jobs(out: str, flags, verbose: bool = False):
+    """The compile commands of one library build (one object per source, each with its own flags)
+    and its link command.  Objects go to <out>.objs/ (git- and gpurun-ignored)."""
+    odir = out + ".objs"
+    os.makedirs(odir, exist_ok=True)
+    objs, comp = [], []
+    for f in SRCS:
+        o = os.path.join(odir, f.rsplit(".", 1)[0] + ".o")
+        objs.append(o)
+        comp.append(([HIPCC, f"--offload-arch={ARCH}", *COMMON, *flags, *FILE_FLAGS.get(f, []), "-c", "-o", o,
+                      os.path.join(CSRC, f)], verbose and f == "td_kernels.hip"))
+    link = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", out, *objs]
+    return comp, link
+
+
+def build_lib(out: str, flags, verbose: bool = False) -> None:
+    """One library from the sources with extra flags (scripts/build_variants.sh)."""
+    comp, link = lib_jobs(out, flags, verbose)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=_workers(len(comp))) as ex:
+        for f in [ex.submit(_run_hip, cmd, v) for cmd, v in comp]:
+            f.result()
+    _run(link)
+
+
 def build(force: bool = False, verbose: bool = False, extra: bool = True) -> None:
     """The product library, the compat layer and the drop-in driver.  extra: also the two test /
     diagnostic builds of the same sources (libturbo_mi355x_redo.so, which every log-MAP alpha window
     takes the speculation's exact redo in, for test_alpha_speculation_redo_path_is_exact; and the
     stamps build for scripts/diag_stamps.py).  __graft_entry__.build() asks for them, as the GPU
     tests load the redo build."""
-    srcs = [os.path.join(CSRC, f) for f in ("td_kernels.hip", "td_kernels_w12.hip", "td_synth.hip", "td_api.cpp")]
-    deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h")]
+    srcs = [os.path.join(CSRC, f) for f in SRCS]
+    deps = srcs + [os.path.join(CSRC, f) for f in ("td_kernels.h", "td_tables.h")] + [os.path.join(INC, "turbo_mi355x.h"),
+                                                                                       __file__]
     stamps = os.path.join(PKG, "libturbo_mi355x_stamps.so")   # diagnostic build (phase cycle stamps)
     redo = os.path.join(PKG, "libturbo_mi355x_redo.so")       # test build: every log-MAP alpha window takes
-    jobs = []                                                  # the speculation's exact redo (test_gpu_decode)
+    comp, links = [], []                                       # the speculation's exact redo (test_gpu_decode)
     for out, flags in ((LIB, []), (stamps, ["-DTD_STAMPS"]), (redo, ["-DTD_ASPEC_REDO"])):
         if out != LIB and not extra:
             continue
         if force or _newer(out, deps):
-            jobs.append(([HIPCC, f"--offload-arch={ARCH}", *COMMON, *flags, "-shared", "-o", out, *srcs], verbose and out == LIB))
-    # the builds are independent: run them side by side, as memory allows
-    with concurrent.futures.ThreadPoolExecutor(max_workers=_workers(len(jobs) or 1)) as ex:
-        for f in [ex.submit(_run_hip, cmd, v) for cmd, v in jobs]:
+            c, l = lib_jobs(out, flags, verbose and out == LIB)
+            comp += c
+            links.append(l)
+    # the compiles are independent: run them side by side, as memory allows
+    with concurrent.futures.ThreadPoolExecutor(max_workers=_workers(len(comp) or 1)) as ex:
+        for f in [ex.submit(_run_hip, cmd, v) for cmd, v in comp]:
             f.result()
+    for l in links:
+        _run(l)
     csrc = os.path.join(CSRC, "log_map_compat.cpp")
     if os.path.exists(csrc) and (force or _newer(COMPAT, [csrc, LIB, os.path.join(INC, "turbo_mi355x.h")])):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-shared", "-o", COMPAT, csrc,

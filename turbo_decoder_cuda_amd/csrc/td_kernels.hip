@@ -2223,6 +2223,9 @@ __global__ __launch_bounds__(kWaves * 64, 2) void siso_kernel(DecodeParams<T> p,
     wg_release(w, p.cu_slots);
 }
 
+#ifdef TD_WIN_TU
+// The sub-block schedule is compiled in its own translation unit (td_kernels_win.hip, built with the
+// max-ILP machine scheduler: build.py WIN_FLAGS); td_kernels.hip and td_kernels_w12.hip skip it.
 // ================================================================== sub-block schedule
 // BASELINE config 5 / SURVEY.md 8f row 3: the trellis of each codeword is cut into nS sub-blocks
 // of W steps (the last one also takes the remainder, e.g. the 3 tail steps) decoded in parallel.
@@ -3183,6 +3186,8 @@ hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const 
     return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st, ws) : launch_window_algo<T, 0>(p, w, wb, st, ws);
 }
 
+#endif  // TD_WIN_TU
+
 constexpr int kDemuxBlocks = 32768;   // grid cap of demux_kernel (grid-stride loop beyond); 8192: 0.230 ms, 32768: 0.212 (config 2)
 
 // Demultiplex + x0.5 (log_map.cpp:1202-1205, 1083-1127) of the reference stream layout into the
@@ -3428,16 +3433,10 @@ hipError_t launch_siso(const DecodeParams<T>& p, const T* recs, const T* la, T* 
     return hipGetLastError();
 }
 
-#ifndef TD_W12_TU
+#if !defined(TD_W12_TU) && !defined(TD_WIN_TU)
 template hipError_t launch_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
-template hipError_t launch_window_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
-template hipError_t launch_window_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
 template hipError_t launch_turbo<double>(const DecodeParams<double>&, hipStream_t, bool);
-template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, const WindowBufs<double>&,
-                                         hipStream_t, const WindowStreams&);
-template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, const WindowBufs<float>&,
-                                        hipStream_t, const WindowStreams&);
 template hipError_t launch_turbo<float>(const DecodeParams<float>&, hipStream_t, bool);
 template hipError_t launch_siso<double>(const DecodeParams<double>&, const double*, const double*, double*, int,
                                         double*, hipStream_t);
@@ -3445,6 +3444,14 @@ template hipError_t launch_siso<float>(const DecodeParams<float>&, const float*,
                                        hipStream_t);
 
 int window_steps() { return kW; }
+#endif
+#ifdef TD_WIN_TU
+template hipError_t launch_window_demux<double>(const DecodeParams<double>&, const double*, hipStream_t);
+template hipError_t launch_window_demux<float>(const DecodeParams<float>&, const float*, hipStream_t);
+template hipError_t launch_window<double>(const DecodeParams<double>&, const WindowParams&, const WindowBufs<double>&,
+                                         hipStream_t, const WindowStreams&);
+template hipError_t launch_window<float>(const DecodeParams<float>&, const WindowParams&, const WindowBufs<float>&,
+                                        hipStream_t, const WindowStreams&);
 #endif
 
 }  // namespace td / td_w12
