@@ -587,6 +587,16 @@ __device__ __forceinline__ void dma16(unsigned lds, const void* src)
                  : "memory");
 }
 
+// One 4-byte element per lane, HBM -> LDS at lds + 4 * lane (as dma16)
+__device__ __forceinline__ void dma4(unsigned lds, const void* src)
+{
+    unsigned save;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "s"(lds), "v"(src)
+                 : "memory");
+}
+
 // dma16 with sc0 sc1 nt on the load: the alpha copies, whose lines are read once -- not keeping them
 // in L2 / MALL leaves those to the other streams.  Measured (config 2, one box, 2 rounds): nt 16.95 /
 // 16.91 ms, sc0 sc1 nt 16.94 / 16.88, sc1 17.15 / 17.22, against 17.14 / 17.21 without.  The same bits
@@ -2725,6 +2735,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
     __shared__ alignas(16) T ck_lds[4 * 8 * 64];   // per wave: the next segment's checkpoint (DMA slot)
     __shared__ alignas(16) T in_lds[4 * 3 * S * 64];   // per wave: the next segment's ys, yp, La rows (DMA slot)
+    __shared__ alignas(16) int ix_lds[4 * 64];         // per wave: the next segment's interleaver entries (DMA slot)
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
@@ -2797,15 +2808,15 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     static_assert(S * kRowBytes % 1024 == 0, "whole 1 KB DMA chunks");
     int bp = base0 + floor_div(pe - base0, S) * S;
     // the segment's interleaver entries (wave-uniform: scalar loads), one segment ahead
-    int npm[S], npk[S];
+    int* const ixslot = ix_lds + wave * 64;                           // the next segment's perm / pi entries
+    const unsigned ixslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(ixslot));
     auto prefetch = [&](int nbp) {
-#pragma unroll
-        for (int m = 0; m < S; ++m) {
-            const int q = min(nbp + m, K - 1);
-            npm[m] = perm[q];
-            npk[m] = pi[q];
-        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // the slots' previous reads are done
+        // The interleaver entries by DMA too (lane l < S: perm, S <= l < 2S: pi, of position nbp + l % S),
+        // waited for with the rest at the next segment's start.  As scalar loads they were waited out at
+        // the lgkmcnt(0) above or at the first table read after it (scalar loads complete out of order,
+        // so while one is in flight every LDS wait of the wave is an lgkmcnt(0)).
+        dma4(ixslot_lds, (lane & S ? pi : perm) + min(nbp + (lane & (S - 1)), K - 1));
         const int ns = seg_sub(nbp), nst = ns * W;
         if (nbp >= base0 && nbp < sw_end(ns, nS, W, L)) {
             const char* src = reinterpret_cast<const char*>(sw_ck(a, t, ns, (nbp - nst) / S) - lane) + lane * 16;
@@ -2862,8 +2873,8 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             r.yp = inslot[(S + m) * 64 + lane];
             r.la = inslot[(2 * S + m) * 64 + lane];
             x[m] = sw_cvt(r, bp + m < a.la_len);
-            pm[m] = npm[m];
-            pk[m] = npk[m];
+            pm[m] = __builtin_amdgcn_readfirstlane(ixslot[m]);
+            pk[m] = __builtin_amdgcn_readfirstlane(ixslot[S + m]);
             dst[m] = false;
             dpm[m] = pm[m];
             dpk[m] = pk[m];
