@@ -185,8 +185,10 @@ def test_three_workgroups_per_cu(monkeypatch, precision, algo, K, f1, f2, B):
     assert np.array_equal(le2.view(np.uint8), le3.view(np.uint8))
     assert np.array_equal(fast2, fast3) and np.array_equal(fast3, bits3)
     oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
-    for b in range(0, B, 307 if K == 40 else 1201):
-        ob, ol = O.turbo_decode(np.asarray(flow[b], dtype=np.float64), K, f1, f2, iters, algo=oalgo)
+    # the oracle sample: every 41st (K = 40) / 193rd (K = 1024) codeword and the last one, so every
+    # dispatch round and the partial last group are covered (122-151 / 33 codewords)
+    for b in list(range(0, B, 41 if K == 40 else 193)) + [B - 1]:
+        ob, ol = O.turbo_decode(np.ascontiguousarray(flow[b]), K, f1, f2, iters, algo=oalgo)   # fp32: its restatement
         if precision == "f64":
             assert np.array_equal(bits3[b], ob.astype(np.uint8)), f"codeword {b}"
             assert np.abs(le3[b] - ol).max() <= 1e-9, f"codeword {b}"
@@ -256,7 +258,8 @@ def test_full_size_f32_large_batch(monkeypatch):
     """Config 4's per-GPU shard size in fp32 (B = 32768, K = 6144, 8 iterations, 1.0 dB, the
     device generator's frames of srand(20261015)): the occupancy pick runs four workgroups per CU
     (turbo_decode_kernel4); its hard bits equal the two-per-CU kernel's (TD_OCC3=0) and recover
-    every info bit, in log-MAP and Max-Log-MAP."""
+    every info bit, in log-MAP and Max-Log-MAP; six codewords across its dispatch rounds equal the
+    oracle's fp32 restatement."""
     import torch
 
     from turbo_decoder_cuda_amd import TurboCodec
@@ -276,6 +279,13 @@ def test_full_size_f32_large_batch(monkeypatch):
                 torch.cuda.synchronize()
         assert torch.equal(out["1"], out["0"]), algo
         assert int((out["1"] != u).sum().item()) == 0, algo
+        # parity, not only self-consistency: a sample spread over the four-per-CU kernel's dispatch
+        # rounds against the oracle's fp32 restatement (converged frames: equal bits)
+        sample = [0, 4097, 12345, 20000, 28671, 32767]
+        xs = np.ascontiguousarray(x[sample].cpu().numpy())
+        ob = O.decode_batch(xs, K, f1, f2, 8, algo=O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP,
+                            nthreads=6)
+        assert np.array_equal(ob, out["1"][sample].cpu().numpy()), algo
 
 
 def test_le_dump_layout_against_golden():
