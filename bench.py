@@ -134,6 +134,10 @@ def load_traffic_rec(cfg_key):
 
 
 N_SIMDS = 1024   # 256 CUs x 4 SIMDs (MI355X)
+# The VALU issue fraction the windowed kernels' own arithmetic reaches with no memory traffic at their
+# occupancy (two waves per SIMD): scripts/ubench_window.hip, beta-position mix (alpha recompute + beta
+# step + LLR folds), profiles/r05/ubench_window.jsonl (0.754; the alpha mix 0.762; three waves 0.809).
+WINDOW_ISSUE_CEILING = 0.754
 
 
 def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
@@ -168,7 +172,12 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
                     "pmc_source": rec.get("source"), "kernel": rec.get("kernel")})
         floor = max(out["valu_floor_ms"], out["hbm_floor_ms"])
         out.update({"binding": "valu" if out["valu_floor_ms"] >= out["hbm_floor_ms"] else "hbm",
-                    "frac_of_binding": round(floor / decode_ms, 4)})
+                    "frac_of_binding": round(floor / decode_ms, 4),
+                    # the same VALU fraction against the issue rate the kernels' instruction mix reaches
+                    # at their occupancy in the microbenchmark (a measured ceiling, not a spec)
+                    "valu_issue_ceiling": WINDOW_ISSUE_CEILING,
+                    "valu_issue_ceiling_source": "scripts/ubench_window.hip, 2 waves/SIMD (profiles/r05/ubench_window.jsonl)",
+                    "frac_of_issue_ceiling": round(out["valu_issue_frac"] / WINDOW_ISSUE_CEILING, 4)})
     return out
 
 

@@ -121,3 +121,4 @@ def test_window_roofline_record():
     assert r["binding"] == ("valu" if r["valu_floor_ms"] >= r["hbm_floor_ms"] else "hbm")
     assert abs(r["frac_of_binding"] - floor / 80.0) < 1e-3
     assert 0 < r["valu_issue_frac"] < 1 and 0 < r["traffic_frac"] < 1
+    assert abs(r["frac_of_issue_ceiling"] - r["valu_issue_frac"] / bench.WINDOW_ISSUE_CEILING) < 1e-3
