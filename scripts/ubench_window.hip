@@ -3,7 +3,8 @@
 // three-table max* layout (SwLut: 32 columns, thr / vlo / vhi), inputs read from LDS per step, no HBM.
 //   MIX 0: the alpha kernel's core -- one alpha step a position (8 max*), normalised every 4;
 //   MIX 1: the beta kernel's core -- per position one alpha-recompute step, one beta step and the LLR's
-//          two 7-deep left folds (log_map.cpp:1024-1039), both chains normalised every 4.
+//          two 7-deep left folds (log_map.cpp:1024-1039), both chains normalised every 4;
+//   MIX 2, 3: mixes 0, 1 on a two-read table layout (threshold + a 16-byte (lo, hi) pair).
 // Each mix runs at WPS = 1, 2, 3 waves per SIMD (one workgroup of 4 x WPS waves on each of the 256 CUs,
 // held to one a CU by LDS padding), so the issue rate at the beta kernel's two waves per SIMD can be read
 // against one and three.  Prints per-wave cycles per position; a PMC pass (SQ_INSTS_VALU) gives the
@@ -29,15 +30,26 @@ constexpr int kOffV = kTab + 8, kOffH = 2 * kOffV + 8, kLutBytes = kOffH + kTab;
 constexpr int kInSteps = 16;   // input rows cycled through (P, Q per lane)
 constexpr int kPos = 4096;     // positions a wave steps
 
-__device__ __forceinline__ double mstar(double x, double y, const char* lut)
+// LAY 0: three tables (the kernels' SwLut), three ds_read_b64 a max*.  LAY 1: the threshold table and
+// a (lo, hi) pair table of 16-byte entries [bucket][32 columns], two reads a max* (ds_read_b64 +
+// ds_read_b128; the b128 read groups {0-3,12-15,20-27}, ... hit distinct banks for any buckets).
+constexpr int kPairOff = (kLutBytes + 15) & ~15;   // pair table: 512-byte rows after the three tables, 16-B aligned
+template <int LAY>
+__device__ __forceinline__ double mstar(double x, double y, const char* lut, const char* lutp)
 {
     const double d = y - x;
     const unsigned hi = (unsigned)((unsigned long long)__double_as_longlong(d) >> 32);
     int q = (int)__builtin_amdgcn_ubfe(hi, BucketBits<double>::shift, BucketBits<double>::width);
     q = min(max(q, BucketBits<double>::base), BucketBits<double>::base + kLutSize - 1);
-    const char* r = lut + q * kRow;
-    const double thr = *(const double*)r, lo = *(const double*)(r + kOffV), hv = *(const double*)(r + kOffH);
-    return fmax(x, y) + (fabs(d) >= thr ? hv : lo);
+    if constexpr (LAY == 0) {
+        const char* r = lut + q * kRow;
+        const double thr = *(const double*)r, lo = *(const double*)(r + kOffV), hv = *(const double*)(r + kOffH);
+        return fmax(x, y) + (fabs(d) >= thr ? hv : lo);
+    } else {
+        const double thr = *(const double*)(lut + q * kRow);
+        const double2 v = *(const double2*)(lutp + q * (2 * kRow));
+        return fmax(x, y) + (fabs(d) >= thr ? v.y : v.x);
+    }
 }
 
 __device__ __forceinline__ double g(double P, double Q, int s) { return kTrellisQ[s] ? Q : P; }
@@ -49,20 +61,26 @@ __device__ __forceinline__ void norm(double (&v)[8])
     for (int j = 0; j < 8; ++j) v[j] -= m;
 }
 
-template <int MIX, int WPS>
+template <int MIX_, int WPS>
 __global__ __launch_bounds__(256 * WPS) void ub(const double* __restrict__ lut_g, const double* __restrict__ in_g,
                                                double* out, unsigned long long* clk)
 {
-    __shared__ alignas(16) char lut_s[kLutBytes];
+    constexpr int MIX = MIX_ & 1, LAY = MIX_ >> 1;
+    __shared__ alignas(16) char lut_s[kPairOff + kRows * 2 * kRow];
     __shared__ alignas(16) double in_s[kInSteps * 2 * 64];
     for (int e = threadIdx.x; e < 3 * kRows * kCols; e += blockDim.x) {
         const int t = e / (kRows * kCols), o = e % (kRows * kCols);
         *(double*)(lut_s + (t == 0 ? 0 : t == 1 ? kOffV : kOffH) + o * 8) = lut_g[e];
     }
+    for (int e = threadIdx.x; e < kRows * kCols; e += blockDim.x) {   // pair table (lo, hi) from tables 1, 2
+        *(double*)(lut_s + kPairOff + e * 16) = lut_g[kRows * kCols + e];
+        *(double*)(lut_s + kPairOff + e * 16 + 8) = lut_g[2 * kRows * kCols + e];
+    }
     for (int e = threadIdx.x; e < kInSteps * 2 * 64; e += blockDim.x) in_s[e] = in_g[e];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const char* lut = lut_s + (lane % kCols) * 8 - BucketBits<double>::base * kRow;
+    const char* lutp = lut_s + kPairOff + (lane % kCols) * 16 - BucketBits<double>::base * 2 * kRow;
     double a[8], b[8], acc = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -84,18 +102,18 @@ __global__ __launch_bounds__(256 * WPS) void ub(const double* __restrict__ lut_g
                     t0[j] = (a[p0] - g(P, Q, p0)) + b[j];
                     t1[j] = (a[p1] + g(P, Q, p1)) + b[j];
                 }
-                double r0 = mstar(t0[0], t0[1], lut), r1 = mstar(t1[0], t1[1], lut);
+                double r0 = mstar<LAY>(t0[0], t0[1], lut, lutp), r1 = mstar<LAY>(t1[0], t1[1], lut, lutp);
 #pragma unroll
                 for (int j = 2; j < 8; ++j) {
-                    r0 = mstar(r0, t0[j], lut);
-                    r1 = mstar(r1, t1[j], lut);
+                    r0 = mstar<LAY>(r0, t0[j], lut, lutp);
+                    r1 = mstar<LAY>(r1, t1[j], lut, lutp);
                 }
                 acc += r1 - r0;
                 double nb[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const double G = g(P, Q, j);
-                    nb[j] = mstar(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut);
+                    nb[j] = mstar<LAY>(b[kTrellisNext[j][0]] - G, b[kTrellisNext[j][1]] + G, lut, lutp);
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) b[j] = nb[j];
@@ -103,7 +121,7 @@ __global__ __launch_bounds__(256 * WPS) void ub(const double* __restrict__ lut_g
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int p0 = kTrellisLast[j][0], p1 = kTrellisLast[j][1];
-                n[j] = mstar(a[p0] - g(P, Q, p0), a[p1] + g(P, Q, p1), lut);
+                n[j] = mstar<LAY>(a[p0] - g(P, Q, p0), a[p1] + g(P, Q, p1), lut, lutp);
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) a[j] = n[j];
@@ -185,6 +203,8 @@ int main()
     run<1, 1>(dl, di, dout, dclk);
     run<1, 2>(dl, di, dout, dclk);
     run<1, 3>(dl, di, dout, dclk);
+    run<2, 2>(dl, di, dout, dclk);   // the two mixes on the (thr, pair) layout
+    run<3, 2>(dl, di, dout, dclk);
     hipFree(dl);
     hipFree(di);
     hipFree(dout);

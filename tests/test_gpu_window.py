@@ -106,6 +106,34 @@ def test_window_vs_c_restatement(monkeypatch, K, f1, f2, W, g, nii, conc, scale,
         assert np.abs(le[b] - ol).max() <= 1e-9, f"codeword {b}"
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("K,f1,f2,W,g,nii,conc,scale", [
+    (1024, 31, 64, 64, 30, False, False, 1.0),
+    (512, 31, 64, 48, 48, True, True, 0.77),
+    (200, 13, 50, 50, 9, True, True, 0.77),       # W not a multiple of the segment
+    (160, 21, 120, 64, 192, True, True, 1.0),     # overlap beyond both ends
+    (6144, 263, 480, 64, 30, False, False, 1.0),  # the drop-in's opt-in schedule at config 5's K
+])
+def test_window_single_frame_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale, algo, precision):
+    """A batch of one codeword (the drop-in's frame) takes the beta kernel's lane-fold variant (the S
+    LLRs of a segment folded side by side, one per lane): bits identical to the C restatement, Le
+    within 1e-9 (fp64) / relative 1e-4 (fp32), every iteration, for two frames decoded one at a time."""
+    iters = 3 if K > 2048 else 5
+    _, flow = O.synth_batch(K, f1, f2, 0.3, 5 + W + g, 2)
+    if precision == "f32":
+        flow = flow.astype(np.float32)
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    for b in range(2):
+        bits, le = _decode(K, f1, f2, iters, flow[b:b + 1], algo, W, g, precision=precision, ext_scale=scale,
+                           nii=nii, concurrent=conc)
+        ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo, nii=nii, concurrent=conc,
+                                       scale=scale)
+        assert np.array_equal(bits[0], ob), f"frame {b}"
+        tol = 1e-9 if precision == "f64" else 1e-4 * max(1.0, np.abs(ol).max())
+        assert np.abs(le[0] - ol).max() <= tol, f"frame {b}"
+
+
 @pytest.mark.parametrize("algo", ["logmap", "maxlog"])
 @pytest.mark.parametrize("run", [0, 3])
 def test_window_f32_vs_c_restatement(monkeypatch, algo, run):

@@ -2728,7 +2728,11 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
 #else
 #define TD_SW_BETA_ATTR
 #endif
-template <typename T, int ALGO, int S>
+// LF (lane folds; a batch of one codeword, the drop-in's frame): every lane of the wave runs codeword
+// 0's chains, and the S LLRs of a segment are folded side by side, position m in lane m, once the
+// segment's beta steps are done -- one fold latency a segment instead of S (the folds are the beta
+// kernel's longest dependent chains: 2 x 7 table max* a position).  Same operations, same order.
+template <typename T, int ALGO, int S, bool LF>
 __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
                                                       const int* __restrict__ pinv)
 {
@@ -2741,7 +2745,9 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
     const char* lut = sw_lut_lane<T>(lut_s, lane);
-    const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, cwv = t.cwv, b = t.b;
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, cwv = t.cwv;
+    const int col = LF ? 0 : lane;                // this lane's codeword within the wave
+    const int b = LF ? t.cwv * 64 : t.b;
     T* const niw = a.nii_wr + ((size_t)dec * a.Bp + b) * nS * 16;
     const T* const nir = a.nii_rd + ((size_t)dec * a.Bp + b) * nS * 16;
     const bool use_nii = a.nii && a.it > 0;
@@ -2749,7 +2755,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     const int* const perm = dec ? pi : pinv;
     T* const le = a.le[dec] + (size_t)cwv * K * kSwCw;
     uint8_t* const bitsT = dec ? a.bitsT : nullptr;
-    const int bcol = t.cwv * 64 + lane;
+    const int bcol = LF ? t.cwv * 64 : t.cwv * 64 + lane;
     // clock sample (as turbo_decode_kernel's): workgroup 0's shader clock and 100 MHz counter at its
     // start and end, two scalar reads each, written by its first lane with one vector store
     const bool clk = a.clk && p.clk && blockIdx.x == 0;
@@ -2842,13 +2848,24 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     bool dst[S];
 #pragma unroll
     for (int m = 0; m < S; ++m) dst[m] = false;
+    // LF: lane m < S keeps position m's extrinsic, decision and write positions
+    T lf_lev = 0;
+    int lf_bit = 0, lf_pm = 0, lf_pk = 0, cur_pm = 0, cur_pk = 0;
+    bool lf_st = false;
     auto flush = [&] {
-#pragma unroll
-        for (int m = 0; m < S; ++m)
-            if (dst[m] && t.live) {
-                le[(size_t)dpm[m] * kSwCw + lane] = dlev[m];
-                if (bitsT) bitsT[(size_t)dpk[m] * a.Bp + bcol] = (uint8_t)dbit[m];
+        if constexpr (LF) {
+            if (lf_st) {
+                le[(size_t)lf_pm * kSwCw] = lf_lev;
+                if (bitsT) bitsT[(size_t)lf_pk * a.Bp + bcol] = (uint8_t)lf_bit;
             }
+        } else {
+#pragma unroll
+            for (int m = 0; m < S; ++m)
+                if (dst[m] && t.live) {
+                    le[(size_t)dpm[m] * kSwCw + lane] = dlev[m];
+                    if (bitsT) bitsT[(size_t)dpk[m] * a.Bp + bcol] = (uint8_t)dbit[m];
+                }
+        }
     };
     int pm[S], pk[S];
     // one position's LLR, extrinsic and decision (beta = beta[pos + 1]), kept for the flush
@@ -2866,12 +2883,17 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
         const bool main = bp < en;                        // the segment lies in sub-block s's own range
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this segment's DMA (and the stores before it)
         flush();
+        if constexpr (LF) {
+            lf_st = false;
+            cur_pm = ixslot[lane & (S - 1)];          // lane m: position m's write positions
+            cur_pk = ixslot[S + (lane & (S - 1))];
+        }
 #pragma unroll
         for (int m = 0; m < S; ++m) {
             SwRaw<T> r;
-            r.ys = inslot[m * 64 + lane];
-            r.yp = inslot[(S + m) * 64 + lane];
-            r.la = inslot[(2 * S + m) * 64 + lane];
+            r.ys = inslot[m * 64 + col];
+            r.yp = inslot[(S + m) * 64 + col];
+            r.la = inslot[(2 * S + m) * 64 + col];
             x[m] = sw_cvt(r, bp + m < a.la_len);
             pm[m] = __builtin_amdgcn_readfirstlane(ixslot[m]);
             pk[m] = __builtin_amdgcn_readfirstlane(ixslot[S + m]);
@@ -2881,7 +2903,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
         }
         if (main)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) as[0][j] = ckslot[j * 64 + lane];
+            for (int j = 0; j < 8; ++j) as[0][j] = ckslot[j * 64 + col];
         if (bp - S >= base0) prefetch(bp - S);
         if (main) {                                       // alpha of the segment from its checkpoint
 #pragma unroll
@@ -2906,11 +2928,26 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             else
                 sw_set(bb, 0, (T)0);
         }
+        T asel[LF ? 8 : 1], bsel[LF ? 8 : 1];           // LF: lane m's position's alpha, beta[pos + 1], inputs
+        SwIn<T> xsel{};
+        bool sel = false;
 #pragma unroll
         for (int m = S - 1; m >= 0; --m) {
             const int pos = bp + m;
             if (pos > pe) continue;
-            if (main && pos < en) llr_out(pos, as[m], x[m], m);
+            if constexpr (LF) {
+                if (main && pos < en && lane == m) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        asel[j] = as[m][j];
+                        bsel[j] = be[j];
+                    }
+                    xsel = x[m];
+                    sel = true;
+                }
+            } else if (main && pos < en) {
+                llr_out(pos, as[m], x[m], m);
+            }
             const bool doB = hasB && pos < qb;
             if (doB)
                 sw_beta_step2<T, ALGO>(be, bb, x[m], lut);
@@ -2923,6 +2960,21 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             if (s > 0 && pos == nb && t.live)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) niw[(size_t)(s - 1) * 16 + 8 + j] = be[j];
+        }
+        if constexpr (LF) {                               // the segment's S folds, one per lane
+            if (!sel)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) asel[j] = bsel[j] = (T)0;   // (computed and dropped)
+            const T llr = sw_llr<T, ALGO>(asel, bsel, xsel, lut);
+            const T lev = (llr - xsel.la - (T)2 * xsel.ys) * a.ext_scale;
+            const int pos = bp + lane;
+            lf_lev = lev;
+            lf_bit = llr < (T)0 ? 0 : 1;
+            lf_pm = cur_pm;
+            lf_pk = cur_pk;
+            lf_st = sel && pos < K && b < p.B;
+            if (p.le_dump && sel && b < p.B)
+                p.le_dump[(size_t)b * p.iters * 2 * L + (size_t)(2 * a.it + dec) * L + pos] = lev;
         }
         if (hasB && bp == st) {                           // hand over to sub-block s-1
             if (qb <= st) {                               // g = 0: its chain starts at its end
@@ -3152,7 +3204,12 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                     if (e != hipSuccess) return e;
                     recorded[h + 1] = true;
                 }
-                hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S>), dim3(q.blocks), dim3(256), 0, q.s, p, a, p.pi, p.pinv);
+                if (p.B == 1)   // the drop-in's single frame: lane folds
+                    hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S, true>), dim3(q.blocks), dim3(256), 0, q.s, p, a, p.pi,
+                                       p.pinv);
+                else
+                    hipLaunchKernelGGL((sw_beta_kernel<T, ALGO, S, false>), dim3(q.blocks), dim3(256), 0, q.s, p, a, p.pi,
+                                       p.pinv);
                 hipError_t e = check();
                 if (e != hipSuccess) return e;
             }
