@@ -2719,6 +2719,166 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
     }
 }
 
+// ---- alpha for a batch of one codeword (the drop-in's frame): the chain's 8 states across 8 lanes
+// (state j in lane j of each group of 8 lanes; the groups mirror each other, lanes 0-7 store), the two
+// predecessors fetched by ds_bpermute.  A lone sw_alpha_kernel wave issues a step's 8 max* from one lane
+// (about 650 cycles a step); here each lane does one.  Per state the operations and their order are
+// sw_alpha_step's; the normalising max (sw_normalise) is exact in any order.
+template <typename T>
+__device__ __forceinline__ T sw_lane_get(T v, int src)   // v of lane src
+{
+    if constexpr (sizeof(T) == 8) {
+        const long long w = __double_as_longlong((double)v);
+        const int lo = __builtin_amdgcn_ds_bpermute(src * 4, (int)w);
+        const int hi = __builtin_amdgcn_ds_bpermute(src * 4, (int)(w >> 32));
+        return (T)__longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+    } else {
+        return (T)__int_as_float(__builtin_amdgcn_ds_bpermute(src * 4, __float_as_int((float)v)));
+    }
+}
+constexpr unsigned sw_pack_last(int u)   // kTrellisLast[.][u] as 8 nibbles (runtime-indexable)
+{
+    unsigned r = 0;
+    for (int j = 0; j < 8; ++j) r |= (unsigned)kTrellisLast[j][u] << (4 * j);
+    return r;
+}
+constexpr unsigned sw_pack_q()           // kTrellisQ as 8 bits
+{
+    unsigned r = 0;
+    for (int j = 0; j < 8; ++j) r |= (kTrellisQ[j] ? 1u : 0u) << j;
+    return r;
+}
+constexpr unsigned kSwLast0 = sw_pack_last(0), kSwLast1 = sw_pack_last(1), kSwQ = sw_pack_q();
+struct SwLps {
+    int j, p0, p1;   // this lane's state; its two predecessors' lanes
+    bool q0, q1;     // their gammas take Q (kTrellisQ)
+};
+template <typename T, int ALGO>
+__device__ __forceinline__ T sw_lps_step(T v, const SwIn<T>& x, const SwLps& l, const char* lut)
+{
+    const T u0 = sw_lane_get(v, l.p0), u1 = sw_lane_get(v, l.p1);
+    return sw_mstar<T, ALGO>(u0 - (l.q0 ? x.Q : x.P), u1 + (l.q1 ? x.Q : x.P), lut);
+}
+template <typename T>
+__device__ __forceinline__ T sw_lps_norm(T v, int lane)
+{
+    T m = vmax(v, sw_lane_get(v, lane ^ 1));
+    m = vmax(m, sw_lane_get(m, lane ^ 2));
+    m = vmax(m, sw_lane_get(m, lane ^ 4));
+    return v - m;
+}
+
+template <typename T, int ALGO, int S>
+__global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, WinArgs<T> a)
+{
+    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
+    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    SwTask t;
+    if (!sw_task(p, a, t)) return;
+    const int lane = threadIdx.x & 63;
+    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    SwLps l;
+    l.j = lane & 7;
+    l.p0 = (lane & ~7) + (int)((kSwLast0 >> (4 * l.j)) & 7);
+    l.p1 = (lane & ~7) + (int)((kSwLast1 >> (4 * l.j)) & 7);
+    l.q0 = (kSwQ >> (l.p0 & 7)) & 1;
+    l.q1 = (kSwQ >> (l.p1 & 7)) & 1;
+    const int W = a.W, g = a.g, nS = a.nS, L = p.L, dec = t.dec, cwv = t.cwv, b0 = cwv * 64;
+    const bool wr = lane < 8 && b0 < p.B;          // lanes 0-7 store codeword 0's states
+    T* const niw = a.nii_wr + ((size_t)dec * a.Bp + b0) * nS * 16;
+    const T* const nir = a.nii_rd + ((size_t)dec * a.Bp + b0) * nS * 16;
+    const bool use_nii = a.nii && a.it > 0;
+    const int base0 = t.s0 * W;
+    auto set = [&](bool slot0_only, T x0) -> T { return (l.j == 0 || !slot0_only) ? x0 : (T)-kInfty; };
+    auto load_nii = [&](const T* src) -> T {
+        T v = src[l.j];
+        asm volatile("" ::"v"(v));
+        return v;
+    };
+
+    T al, bl;
+    const int i0 = base0 - g;
+    if (i0 <= 0)
+        al = set(true, (T)0);
+    else if (use_nii)
+        al = load_nii(nir + (size_t)t.s0 * 16);
+    else
+        al = set(false, (T)0);
+    bl = set(false, (T)0);
+    const int ps = max(i0, 0);
+
+    int s = t.s0, st = 0, en = 0, qb = 0, need = 0;
+    bool hasB = false;
+    auto enter = [&](int ns) {
+        s = ns;
+        st = s * W;
+        en = sw_end(s, nS, W, L);
+        hasB = s + 1 < t.s1;
+        qb = st + W - g;
+        const int lc = st + ((en - st - 1) / S) * S;
+        need = s < nS - 1 ? max(lc, qb) : lc;
+    };
+    enter(t.s0);
+    if (s < nS - 1 && qb < 0 && wr) niw[(size_t)(s + 1) * 16 + lane] = lane == 0 ? (T)0 : (T)-kInfty;
+    const int stop = [&] {
+        const int sl = t.s1 - 1, stl = sl * W, enl = sw_end(sl, nS, W, L);
+        const int lc = stl + ((enl - stl - 1) / S) * S;
+        return sl < nS - 1 ? max(lc, stl + W - g) : lc;
+    }();
+    auto ck_store = [&](int c) {                     // checkpoint alpha (normalised), column of codeword 0
+        if (wr) (sw_ck(a, t, s, c) - lane)[lane * 64] = al;
+    };
+
+    int bp = base0 + floor_div(ps - base0, S) * S;
+    SwRaw<T> nx[S];
+#pragma unroll
+    for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, 0, bp + m);
+    for (; bp <= stop; bp += S) {
+        SwIn<T> x[S];
+#pragma unroll
+        for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
+#pragma unroll
+        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, 0, bp + S + m);
+        if (hasB && qb >= bp && qb < bp + S && qb >= ps && qb <= stop) {
+            asm volatile("" ::: "memory");
+            if (qb <= 0)
+                bl = set(true, (T)0);
+            else if (use_nii)
+                bl = load_nii(nir + (size_t)(s + 1) * 16);
+            else
+                bl = set(false, (T)0);
+        }
+#pragma unroll
+        for (int m = 0; m < S; ++m) {
+            const int pos = bp + m;
+            if (pos < ps || pos > stop) continue;
+            if (m == 0 && pos >= st && pos < en) ck_store((pos - st) / S);
+            if (s < nS - 1 && pos == qb && wr) niw[(size_t)(s + 1) * 16 + lane] = al;
+            const bool doA = pos < need, doB = hasB && pos >= qb;
+            T na = al, nbv = bl;
+            if (doA) na = sw_lps_step<T, ALGO>(al, x[m], l, lut);
+            if (doB) nbv = sw_lps_step<T, ALGO>(bl, x[m], l, lut);
+            al = na;
+            bl = nbv;
+            if (m == S - 1) {
+                if (doA) al = sw_lps_norm(al, lane);
+                if (doB) bl = sw_lps_norm(bl, lane);
+            }
+        }
+        if (hasB && bp + S == en) {
+            if (qb >= en) {
+                if (wr) niw[(size_t)(s + 1) * 16 + lane] = al;
+                if (use_nii)
+                    bl = load_nii(nir + (size_t)(s + 1) * 16);
+                else
+                    bl = set(false, (T)0);
+            }
+            al = bl;
+            enter(s + 1);
+        }
+    }
+}
+
 // ---- beta + LLR: backward over the run in segments of S positions
 #ifndef TD_SW_BETA_WAVES
 #define TD_SW_BETA_WAVES 0
@@ -3196,7 +3356,10 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 }
                 a.M = q.Ma;
                 a.nR = q.nRa;
-                hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocksa), dim3(256), 0, q.s, p, a);
+                if (p.B == 1)   // the drop-in's single frame: states across lanes
+                    hipLaunchKernelGGL((sw_alpha_lps_kernel<T, ALGO, S>), dim3(q.blocksa), dim3(256), 0, q.s, p, a);
+                else
+                    hipLaunchKernelGGL((sw_alpha_kernel<T, ALGO, S>), dim3(q.blocksa), dim3(256), 0, q.s, p, a);
                 a.M = q.M;
                 a.nR = q.nR;
                 if (h + 1 < nparts && !recorded[h + 1]) {
