@@ -2749,6 +2749,7 @@ constexpr unsigned sw_pack_q()           // kTrellisQ as 8 bits
     return r;
 }
 constexpr unsigned kSwLast0 = sw_pack_last(0), kSwLast1 = sw_pack_last(1), kSwQ = sw_pack_q();
+constexpr int kSwLpsChunk = 128;   // sw_alpha_lps_kernel's input chunk (positions)
 struct SwLps {
     int j, p0, p1;   // this lane's state; its two predecessors' lanes
     bool q0, q1;     // their gammas take Q (kTrellisQ)
@@ -2772,11 +2773,13 @@ template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
     __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
+    __shared__ T lin_s[4][3][kSwLpsChunk];   // per wave: codeword 0's ys, yp, La of a chunk of positions
     if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
     const char* lut = sw_lut_lane<T>(lut_s, lane);
+    T (&lin)[3][kSwLpsChunk] = lin_s[threadIdx.x >> 6];
     SwLps l;
     l.j = lane & 7;
     l.p0 = (lane & ~7) + (int)((kSwLast0 >> (4 * l.j)) & 7);
@@ -2830,15 +2833,30 @@ __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, Wi
     };
 
     int bp = base0 + floor_div(ps - base0, S) * S;
-    SwRaw<T> nx[S];
-#pragma unroll
-    for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, 0, bp + m);
+    // The inputs come a chunk of kSwLpsChunk positions at a time into LDS, every lane loading its share
+    // at once: one memory latency a chunk.  (A lone wave's steps are short enough here that loads issued
+    // one segment ahead were waited for at every segment.)
+    int c0 = bp, c1 = bp;                            // the chunk [c0, c1) in lin
+    auto load_chunk = [&](int from) {
+        c0 = from;
+        c1 = from + kSwLpsChunk;
+        for (int k = lane; k < kSwLpsChunk; k += 64) {
+            const SwRaw<T> r = sw_raw(p, a, dec, cwv, 0, c0 + k);
+            lin[0][k] = r.ys;
+            lin[1][k] = r.yp;
+            lin[2][k] = r.la;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    static_assert(kSwLpsChunk % S == 0, "whole segments a chunk");
     for (; bp <= stop; bp += S) {
+        if (bp >= c1) load_chunk(bp);
         SwIn<T> x[S];
 #pragma unroll
-        for (int m = 0; m < S; ++m) x[m] = sw_cvt(nx[m], bp + m < a.la_len);
-#pragma unroll
-        for (int m = 0; m < S; ++m) nx[m] = sw_raw(p, a, dec, cwv, 0, bp + S + m);
+        for (int m = 0; m < S; ++m) {
+            const SwRaw<T> r{lin[0][bp - c0 + m], lin[1][bp - c0 + m], lin[2][bp - c0 + m]};
+            x[m] = sw_cvt(r, bp + m < a.la_len);
+        }
         if (hasB && qb >= bp && qb < bp + S && qb >= ps && qb <= stop) {
             asm volatile("" ::: "memory");
             if (qb <= 0)
