@@ -4,7 +4,8 @@
 //   MIX 0: the alpha kernel's core -- one alpha step a position (8 max*), normalised every 4;
 //   MIX 1: the beta kernel's core -- per position one alpha-recompute step, one beta step and the LLR's
 //          two 7-deep left folds (log_map.cpp:1024-1039), both chains normalised every 4;
-//   MIX 2, 3: mixes 0, 1 on a two-read table layout (threshold + a 16-byte (lo, hi) pair).
+//   MIX 2, 3: mixes 0, 1 on a two-read table layout (threshold + a 16-byte (lo, hi) pair);
+//   MIX 4, 5: the same two reads from one 1 KiB row a bucket (one row address; thr 2-way conflicted).
 // Each mix runs at WPS = 1, 2, 3 waves per SIMD (one workgroup of 4 x WPS waves on each of the 256 CUs,
 // held to one a CU by LDS padding), so the issue rate at the beta kernel's two waves per SIMD can be read
 // against one and three.  Prints per-wave cycles per position; a PMC pass (SQ_INSTS_VALU) gives the
@@ -45,9 +46,14 @@ __device__ __forceinline__ double mstar(double x, double y, const char* lut, con
         const char* r = lut + q * kRow;
         const double thr = *(const double*)r, lo = *(const double*)(r + kOffV), hv = *(const double*)(r + kOffH);
         return fmax(x, y) + (fabs(d) >= thr ? hv : lo);
-    } else {
+    } else if constexpr (LAY == 1) {
         const double thr = *(const double*)(lut + q * kRow);
         const double2 v = *(const double2*)(lutp + q * (2 * kRow));
+        return fmax(x, y) + (fabs(d) >= thr ? v.y : v.x);
+    } else {   // LAY 2: one 1 KiB row per bucket, [32 columns][thr, pad] then [32 columns][lo, hi]
+        const char* r = lutp + q * (4 * kRow);
+        const double thr = *(const double*)r;
+        const double2 v = *(const double2*)(r + 2 * kRow);
         return fmax(x, y) + (fabs(d) >= thr ? v.y : v.x);
     }
 }
@@ -65,22 +71,32 @@ template <int MIX_, int WPS>
 __global__ __launch_bounds__(256 * WPS) void ub(const double* __restrict__ lut_g, const double* __restrict__ in_g,
                                                double* out, unsigned long long* clk)
 {
-    constexpr int MIX = MIX_ & 1, LAY = MIX_ >> 1;
-    __shared__ alignas(16) char lut_s[kPairOff + kRows * 2 * kRow];
+    constexpr int MIX = MIX_ & 1, LAY = MIX_ >> 1;   // LAY 0, 1, 2
+    __shared__ alignas(16) char lut_s[LAY == 2 ? kRows * 4 * kRow : kPairOff + kRows * 2 * kRow];
     __shared__ alignas(16) double in_s[kInSteps * 2 * 64];
-    for (int e = threadIdx.x; e < 3 * kRows * kCols; e += blockDim.x) {
-        const int t = e / (kRows * kCols), o = e % (kRows * kCols);
-        *(double*)(lut_s + (t == 0 ? 0 : t == 1 ? kOffV : kOffH) + o * 8) = lut_g[e];
-    }
-    for (int e = threadIdx.x; e < kRows * kCols; e += blockDim.x) {   // pair table (lo, hi) from tables 1, 2
-        *(double*)(lut_s + kPairOff + e * 16) = lut_g[kRows * kCols + e];
-        *(double*)(lut_s + kPairOff + e * 16 + 8) = lut_g[2 * kRows * kCols + e];
+    if constexpr (LAY == 2) {
+        for (int e = threadIdx.x; e < kRows * kCols; e += blockDim.x) {   // row q, column c: e = q * 32 + c
+            char* r = lut_s + (e / kCols) * 4 * kRow + (e % kCols) * 16;
+            *(double*)r = lut_g[e];
+            *(double*)(r + 2 * kRow) = lut_g[kRows * kCols + e];
+            *(double*)(r + 2 * kRow + 8) = lut_g[2 * kRows * kCols + e];
+        }
+    } else {
+        for (int e = threadIdx.x; e < 3 * kRows * kCols; e += blockDim.x) {
+            const int t = e / (kRows * kCols), o = e % (kRows * kCols);
+            *(double*)(lut_s + (t == 0 ? 0 : t == 1 ? kOffV : kOffH) + o * 8) = lut_g[e];
+        }
+        for (int e = threadIdx.x; e < kRows * kCols; e += blockDim.x) {   // pair table (lo, hi) from tables 1, 2
+            *(double*)(lut_s + kPairOff + e * 16) = lut_g[kRows * kCols + e];
+            *(double*)(lut_s + kPairOff + e * 16 + 8) = lut_g[2 * kRows * kCols + e];
+        }
     }
     for (int e = threadIdx.x; e < kInSteps * 2 * 64; e += blockDim.x) in_s[e] = in_g[e];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const char* lut = lut_s + (lane % kCols) * 8 - BucketBits<double>::base * kRow;
-    const char* lutp = lut_s + kPairOff + (lane % kCols) * 16 - BucketBits<double>::base * 2 * kRow;
+    const char* lutp = LAY == 2 ? lut_s + (lane % kCols) * 16 - BucketBits<double>::base * 4 * kRow
+                                : lut_s + kPairOff + (lane % kCols) * 16 - BucketBits<double>::base * 2 * kRow;
     double a[8], b[8], acc = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -205,6 +221,8 @@ int main()
     run<1, 3>(dl, di, dout, dclk);
     run<2, 2>(dl, di, dout, dclk);   // the two mixes on the (thr, pair) layout
     run<3, 2>(dl, di, dout, dclk);
+    run<4, 2>(dl, di, dout, dclk);   // and on one 1 KiB row a bucket (thr at a 16-byte column stride)
+    run<5, 2>(dl, di, dout, dclk);
     hipFree(dl);
     hipFree(di);
     hipFree(dout);
