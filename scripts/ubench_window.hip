@@ -164,28 +164,28 @@ void run(const double* lut, const double* in, double* out, unsigned long long* c
     // CU's 160 KiB so that no CU takes two
     const int blocks = 256;
     const size_t dyn = 96 * 1024;
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&ub<MIX, WPS>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ub<MIX, WPS>), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)dyn);
     hipLaunchKernelGGL((ub<MIX, WPS>), dim3(blocks), dim3(256 * WPS), dyn, 0, lut, in, out, clk);   // warm-up
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, 0);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL((ub<MIX, WPS>), dim3(blocks), dim3(256 * WPS), dyn, 0, lut, in, out, clk);
-    hipEventRecord(e1, 0);
+    (void)hipEventRecord(e1, 0);
     if (hipGetLastError() != hipSuccess) std::printf("launch failed\n");
-    hipEventSynchronize(e1);
+    (void)hipEventSynchronize(e1);
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
     unsigned long long c[2];
-    hipMemcpy(c, clk, sizeof c, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(c, clk, sizeof c, hipMemcpyDeviceToHost);
     const double ghz = (double)c[0] / ((double)c[1] / 100e6) / 1e9;   // memrealtime: 100 MHz
     const double cyc = (double)c[0] / kPos;                            // one wave's cycles per position
     std::printf("{\"mix\": %d, \"waves_per_simd\": %d, \"waves\": %d, \"positions\": %d, \"kernel_ms\": %.4f, "
                 "\"sclk_ghz\": %.4f, \"wave_cycles_per_position\": %.1f}\n",
                 MIX, WPS, blocks * 4 * WPS, kPos, ms, ghz, cyc);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
 }
 
 int main()
@@ -207,12 +207,12 @@ int main()
     }
     double *dl, *di, *dout;
     unsigned long long* dclk;
-    hipMalloc(&dl, lut.size() * 8);
-    hipMalloc(&di, in.size() * 8);
-    hipMalloc(&dout, 256 * 3 * 256 * 8);   // 256 workgroups x up to 768 threads
-    hipMalloc(&dclk, 16);
-    hipMemcpy(dl, lut.data(), lut.size() * 8, hipMemcpyHostToDevice);
-    hipMemcpy(di, in.data(), in.size() * 8, hipMemcpyHostToDevice);
+    (void)hipMalloc(&dl, lut.size() * 8);
+    (void)hipMalloc(&di, in.size() * 8);
+    (void)hipMalloc(&dout, 256 * 3 * 256 * 8);   // 256 workgroups x up to 768 threads
+    (void)hipMalloc(&dclk, 16);
+    (void)hipMemcpy(dl, lut.data(), lut.size() * 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(di, in.data(), in.size() * 8, hipMemcpyHostToDevice);
     run<0, 1>(dl, di, dout, dclk);
     run<0, 2>(dl, di, dout, dclk);
     run<0, 3>(dl, di, dout, dclk);
@@ -223,9 +223,9 @@ int main()
     run<3, 2>(dl, di, dout, dclk);
     run<4, 2>(dl, di, dout, dclk);   // and on one 1 KiB row a bucket (thr at a 16-byte column stride)
     run<5, 2>(dl, di, dout, dclk);
-    hipFree(dl);
-    hipFree(di);
-    hipFree(dout);
-    hipFree(dclk);
+    (void)hipFree(dl);
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    (void)hipFree(dclk);
     return 0;
 }
