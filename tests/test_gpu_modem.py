@@ -36,6 +36,27 @@ def test_demodulate_large_random_matches_oracle(M):
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4, 6])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1001])
+def test_demodulate_ragged_and_unaligned(M, n):
+    """Symbol counts around a wave (the staged stores' partial last wave, BPSK's odd count) and
+    buffers 8 bytes off a 16-byte boundary (the 8-byte-access kernel): equal to the oracle."""
+    import torch
+
+    from turbo_decoder_cuda_amd import demodulate
+    rng = np.random.default_rng(100 * M + n)
+    yi, yq = rng.normal(0, 1.2, n), rng.normal(0, 1.2, n)
+    want = O.demodulate(yi, yq, M, 0.83)
+    got = demodulate(torch.from_numpy(yi).cuda(), torch.from_numpy(yq).cuda(), M, 0.83).cpu().numpy()
+    assert np.array_equal(got, want)
+    bi = torch.zeros(n + 1, dtype=torch.float64, device="cuda")
+    bq = torch.zeros(n + 1, dtype=torch.float64, device="cuda")
+    bi[1:] = torch.from_numpy(yi).cuda()
+    bq[1:] = torch.from_numpy(yq).cuda()
+    got = demodulate(bi[1:], bq[1:], M, 0.83).cpu().numpy()   # inputs at +8 bytes
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 6])
 def test_modulate_matches_oracle(M):
     import torch
 
