@@ -2291,6 +2291,7 @@ struct WinArgs {
     T* nii_wr;
     T* ckpt[2];            // per decoder: [nS][Bp/64][ncp][8][64] alpha checkpoints
     uint8_t* bitsT;        // [K][Bp] SISO2's decisions (natural-order rows); null: none this launch
+    uint8_t* bits1;        // B = 1: SISO2's decisions straight into the caller's row (no transpose)
     int clk;               // workgroup 0 of this beta launch samples the clock into p.clk (td_clock_read)
 };
 
@@ -2933,6 +2934,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     const int* const perm = dec ? pi : pinv;
     T* const le = a.le[dec] + (size_t)cwv * K * kSwCw;
     uint8_t* const bitsT = dec ? a.bitsT : nullptr;
+    uint8_t* const bits1 = LF && dec ? a.bits1 : nullptr;
     const int bcol = LF ? t.cwv * 64 : t.cwv * 64 + lane;
     // clock sample (as turbo_decode_kernel's): workgroup 0's shader clock and 100 MHz counter at its
     // start and end, two scalar reads each, written by its first lane with one vector store
@@ -3035,6 +3037,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             if (lf_st) {
                 le[(size_t)lf_pm * kSwCw] = lf_lev;
                 if (bitsT) bitsT[(size_t)lf_pk * a.Bp + bcol] = (uint8_t)lf_bit;
+                if (bits1) bits1[lf_pk] = (uint8_t)lf_bit;
             }
         } else {
 #pragma unroll
@@ -3347,7 +3350,11 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
         a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
         a.nii_wr = wb.nii + (size_t)(it & 1) * nii_half;
         const bool want_bits = p.all_iters || it == p.iters - 1;
-        a.bitsT = want_bits ? wb.bitsT : nullptr;
+        // a single codeword's decisions go straight to its row (sw_beta_kernel<LF>), without the
+        // [K][Bp] staging and bits_transpose_kernel launch (15 a drop-in frame at 15 us each)
+        const bool direct = p.B == 1 && !split;
+        a.bitsT = want_bits && !direct ? wb.bitsT : nullptr;
+        a.bits1 = want_bits && direct ? p.bits + (p.all_iters ? (size_t)it * p.K : 0) : nullptr;
         for (int dec = 0; dec < (w.concurrent ? 1 : 2); ++dec) {
             if (w.concurrent) {   // Jacobi: both SISOs read the other's Le of iteration it-1
                 a.dec = -1;
@@ -3395,7 +3402,7 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
                 if (e != hipSuccess) return e;
             }
         }
-        if (want_bits && (p.all_iters || !split)) {
+        if (want_bits && (p.all_iters || !split) && !direct) {
             const long long stride = p.all_iters ? (long long)p.iters * p.K : p.K;
             hipLaunchKernelGGL(bits_transpose_kernel, dim3((p.K + 63) / 64, a.Bp / 64), dim3(256), 0, st, wb.bitsT,
                                p.K, a.Bp, p.B, p.bits + (p.all_iters ? (size_t)it * p.K : 0), stride);
