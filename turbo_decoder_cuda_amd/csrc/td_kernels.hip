@@ -2292,6 +2292,7 @@ struct WinArgs {
     T* ckpt[2];            // per decoder: [nS][Bp/64][ncp][8][64] alpha checkpoints
     uint8_t* bitsT;        // [K][Bp] SISO2's decisions (natural-order rows); null: none this launch
     uint8_t* bits1;        // B = 1: SISO2's decisions straight into the caller's row (no transpose)
+    int hand;              // B = 1, one sub-block a lane: the alpha kernel runs beta's warm-up (sw_alpha_lps_kernel)
     int clk;               // workgroup 0 of this beta launch samples the clock into p.clk (td_clock_read)
 };
 
@@ -2749,7 +2750,14 @@ constexpr unsigned sw_pack_q()           // kTrellisQ as 8 bits
     for (int j = 0; j < 8; ++j) r |= (kTrellisQ[j] ? 1u : 0u) << j;
     return r;
 }
+constexpr unsigned sw_pack_next(int u)   // kTrellisNext[.][u] as 8 nibbles
+{
+    unsigned r = 0;
+    for (int j = 0; j < 8; ++j) r |= (unsigned)kTrellisNext[j][u] << (4 * j);
+    return r;
+}
 constexpr unsigned kSwLast0 = sw_pack_last(0), kSwLast1 = sw_pack_last(1), kSwQ = sw_pack_q();
+constexpr unsigned kSwNext0 = sw_pack_next(0), kSwNext1 = sw_pack_next(1);
 constexpr int kSwLpsChunk = 128;   // sw_alpha_lps_kernel's input chunk (positions)
 struct SwLps {
     int j, p0, p1;   // this lane's state; its two predecessors' lanes
@@ -2832,6 +2840,24 @@ __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, Wi
     auto ck_store = [&](int c) {                     // checkpoint alpha (normalised), column of codeword 0
         if (wr) (sw_ck(a, t, s, c) - lane)[lane * 64] = al;
     };
+    // a.hand (one sub-block a lane): lanes 8-15 run this sub-block's beta warm-up chain, positions
+    // en + g - 1 down to en, beside alpha -- the same exchange-and-max* step with the beta trellis
+    // (sw_beta_step: b[next0] - G, b[next1] + G, G = gamma of the state), normalised where the beta
+    // kernel normalises it -- and leave beta[en] in column 1 of the sub-block's first checkpoint slot
+    // (unused with one codeword), where sw_beta_kernel<LF> starts from it.
+    const bool hand = a.hand && s < nS - 1;
+    const bool wl = hand && (lane >> 3) == 1;
+    const int nw = hand ? g : 0;
+    int kw = 0;
+    if (wl) {
+        l.p0 = 8 + (int)((kSwNext0 >> (4 * l.j)) & 7);
+        l.p1 = 8 + (int)((kSwNext1 >> (4 * l.j)) & 7);
+        l.q0 = l.q1 = (kSwQ >> l.j) & 1;
+    }
+    if (hand) {
+        const T w0 = use_nii ? nir[(size_t)s * 16 + 8 + l.j] : (T)0;   // the chain of s starts at en + g
+        if (wl) al = w0;
+    }
 
     int bp = base0 + floor_div(ps - base0, S) * S;
     // The inputs come a chunk of kSwLpsChunk positions at a time into LDS, every lane loading its share
@@ -2874,15 +2900,30 @@ __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, Wi
             if (m == 0 && pos >= st && pos < en) ck_store((pos - st) / S);
             if (s < nS - 1 && pos == qb && wr) niw[(size_t)(s + 1) * 16 + lane] = al;
             const bool doA = pos < need, doB = hasB && pos >= qb;
+            const bool wact = kw < nw;
+            const int pw = en + g - 1 - kw;                  // the warm-up chain's position
             T na = al, nbv = bl;
-            if (doA) na = sw_lps_step<T, ALGO>(al, x[m], l, lut);
+            if (doA || wact) {
+                SwIn<T> xs = x[m];
+                if (wact) {
+                    const int iw = min(max(pw - c0, 0), kSwLpsChunk - 1);
+                    const SwRaw<T> r{lin[0][iw], lin[1][iw], lin[2][iw]};
+                    const SwIn<T> xw = sw_cvt(r, pw < a.la_len);
+                    if (wl) xs = xw;
+                }
+                const T n = sw_lps_step<T, ALGO>(al, xs, l, lut);
+                if (wl ? wact : doA) na = n;
+            }
             if (doB) nbv = sw_lps_step<T, ALGO>(bl, x[m], l, lut);
             al = na;
             bl = nbv;
-            if (m == S - 1) {
-                if (doA) al = sw_lps_norm(al, lane);
-                if (doB) bl = sw_lps_norm(bl, lane);
+            const bool nA = m == S - 1 && doA, nW = wact && (pw - base0) % S == 0;
+            if (nA || nW) {
+                const T nv = sw_lps_norm(al, lane);
+                if (wl ? nW : nA) al = nv;
             }
+            if (m == S - 1 && doB) bl = sw_lps_norm(bl, lane);
+            if (wact) ++kw;
         }
         if (hasB && bp + S == en) {
             if (qb >= en) {
@@ -2896,6 +2937,7 @@ __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, Wi
             enter(s + 1);
         }
     }
+    if (wl && b0 < p.B) (sw_ck(a, t, s, 0) - lane)[l.j * 64 + 1] = al;   // beta[en] for sw_beta_kernel<LF>
 }
 
 // ---- beta + LLR: backward over the run in segments of S positions
@@ -2993,6 +3035,16 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
     constexpr int kInDma = S * kRowBytes / 1024;                    // DMA instructions per input array
     static_assert(S * kRowBytes % 1024 == 0, "whole 1 KB DMA chunks");
     int bp = base0 + floor_div(pe - base0, S) * S;
+    if constexpr (LF) {
+        // a.hand: sw_alpha_lps_kernel ran this chain's warm-up and left beta[en] in column 1 of the
+        // sub-block's first checkpoint slot; start at the sub-block's last segment from it
+        if (a.hand && s < nS - 1) {
+            const T* hb = sw_ck(a, t, s, 0) - lane + 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) be[j] = hb[j * 64];
+            bp = en - S;
+        }
+    }
     // the segment's interleaver entries (wave-uniform: scalar loads), one segment ahead
     int* const ixslot = ix_lds + wave * 64;                           // the next segment's perm / pi entries
     const unsigned ixslot_lds = __builtin_amdgcn_readfirstlane(lds_addr(ixslot));
@@ -3345,6 +3397,9 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     }
     auto check = [] { return hipGetLastError(); };
     bool forked[kSwMaxParts] = {}, recorded[kSwMaxParts] = {};
+    // one codeword, one sub-block a lane: beta's warm-up runs in the alpha kernel (sw_alpha_lps_kernel)
+    a.hand = p.B == 1 && !split && part[0].M == 1 && part[0].Ma == 1 && w.overlap > 0 && w.overlap + S <= W &&
+             W % S == 0 && W + 2 * w.overlap + S <= kSwLpsChunk;
     for (int it = 0; it < p.iters; ++it) {
         a.it = it;
         a.nii_rd = wb.nii + (size_t)((it + 1) & 1) * nii_half;
