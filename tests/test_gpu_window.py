@@ -114,6 +114,8 @@ def test_window_vs_c_restatement(monkeypatch, K, f1, f2, W, g, nii, conc, scale,
     (200, 13, 50, 50, 9, True, True, 0.77),       # W not a multiple of the segment
     (160, 21, 120, 64, 192, True, True, 1.0),     # overlap beyond both ends
     (6144, 263, 480, 64, 30, False, False, 1.0),  # the drop-in's opt-in schedule at config 5's K
+    (1024, 31, 64, 64, 30, True, True, 0.77),     # beta warm-up in the alpha kernel, with NII, concurrent
+    (1024, 31, 64, 64, 20, True, False, 1.0),     # the same, serial, another overlap
 ])
 def test_window_single_frame_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale, algo, precision):
     """A batch of one codeword (the drop-in's frame) takes the beta kernel's lane-fold variant (the S
