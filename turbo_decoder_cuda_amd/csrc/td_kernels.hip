@@ -2758,7 +2758,7 @@ constexpr unsigned sw_pack_next(int u)   // kTrellisNext[.][u] as 8 nibbles
 }
 constexpr unsigned kSwLast0 = sw_pack_last(0), kSwLast1 = sw_pack_last(1), kSwQ = sw_pack_q();
 constexpr unsigned kSwNext0 = sw_pack_next(0), kSwNext1 = sw_pack_next(1);
-constexpr int kSwLpsChunk = 128;   // sw_alpha_lps_kernel's input chunk (positions)
+constexpr int kSwLpsChunk = 160;   // sw_alpha_lps_kernel's input chunk (positions): W + 2g + S of config 5 in fp32
 struct SwLps {
     int j, p0, p1;   // this lane's state; its two predecessors' lanes
     bool q0, q1;     // their gammas take Q (kTrellisQ)
