@@ -140,7 +140,7 @@ N_SIMDS = 1024   # 256 CUs x 4 SIMDs (MI355X)
 WINDOW_ISSUE_CEILING = 0.754
 
 
-def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
+def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None):
     """Roofline record of the windowed schedule (BASELINE config 5: fp64 log-MAP, window 64, overlap 30)
     from the live decode time and the committed PMC of the same kernels (profiles/traffic.json key
     K6144_B32768_it8_f64_logmap_w64g30: FETCH_SIZE x2 + WRITE_SIZE bytes and SQ_INSTS_VALU per decode,
@@ -168,7 +168,7 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None):
                     # streams), so the larger floor binds and frac_of_binding = floor / decode time
                     "valu_floor_ms": round(vi * 4.0 / N_SIMDS / (clk * 1e9) * 1e3, 3),
                     "hbm_floor_ms": round(tb / (HBM_MEASURED_GBS * 1e9) * 1e3, 3),
-                    "sclk_ghz": round(clk, 4), "sclk_source": "measured (td_clock_read: one beta workgroup)" if sclk_ghz else "constant",
+                    "sclk_ghz": round(clk, 4), "sclk_source": (sclk_source or "measured (td_clock_read: one beta workgroup)") if sclk_ghz else "constant",
                     "pmc_source": rec.get("source"), "kernel": rec.get("kernel")})
         floor = max(out["valu_floor_ms"], out["hbm_floor_ms"])
         out.update({"binding": "valu" if out["valu_floor_ms"] >= out["hbm_floor_ms"] else "hbm",
@@ -213,7 +213,7 @@ def main():
         codec.set_window(a.window, a.overlap)
     codec.reserve(a.batch)   # also picks the workspace placement (td_reserve)
     placement = codec.placement()
-    placement_cost = codec.placement_cost()
+    placement_cost = codec.placement_cost() + (codec.workspace_bytes(),)
     bits = torch.empty((a.batch, a.K), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -363,6 +363,9 @@ def placement_record(placement, turbo_ms: float, iters: int, cost=None) -> dict:
     if cost and cost[0] is not None and ms:
         rec["search_wall_ms"] = round(cost[0], 1)
         rec["search_peak_gib_held"] = round(cost[1] / 2**30, 2)
+        if len(cost) > 2 and cost[2]:
+            rec["workspace_gib"] = round(cost[2] / 2**30, 3)
+            rec["peak_held_over_workspace"] = round(cost[1] / cost[2], 3)
     if ms and 0 <= kept < len(ms):
         rec["kept_probe_ms"] = ms[kept]
         rec["probe_x_iters_ms"] = round(ms[kept] * iters, 4)
@@ -806,11 +809,17 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         torch.cuda.synchronize(dev)
         steps = max(2, a.steps // 2)
         c.profile(True)
+        # config 5's roofline prices VALU issue at the clock: the amdsmi mean over the whole timed
+        # region, td_clock_read's one-workgroup sample beside it
+        pw = PowerSampler(dev.index) if (win and prec == "f64" and algo == "logmap" and not a.no_power) else None
+        if pw is not None:
+            pw.start()
         t0 = time.perf_counter()
         for _ in range(steps):
             c.decode(x, b, stream=stream)
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
+        prec_pw = pw.stop() if pw is not None else None
         _, kms, _ = c.kernel_ms()
         try:
             vclk = c.clock()[0]
@@ -825,7 +834,11 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B, "config": cfg,
                     "ms_per_step": round(dt / steps * 1e3, 4), "kernel_ms_avg": round(kms, 4), "bit_errors": errs}
         if win and prec == "f64" and algo == "logmap":
-            res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3, vclk)
+            mean_ghz = (prec_pw["sclk_mhz_mean"] / 1e3) if prec_pw and prec_pw.get("sclk_mhz_mean") else None
+            res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3, mean_ghz or vclk,
+                                                   "amdsmi mean over the timed region" if mean_ghz else None)
+            res[key]["roofline"]["sclk_td_clock_read_ghz"] = round(vclk, 4) if vclk else None
+            res[key]["power"] = prec_pw
     if big is not None and a.K == 6144:
         res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
     return res

@@ -70,10 +70,12 @@ int td_reserve(td_handle* h, int B);
  * and keeps the fastest.  Up to TD_PLACEMENT_TRIALS candidates (environment variable, default 24;
  * 1 = a plain allocation); after at least TD_PLACEMENT_MIN candidates (default 8) the search
  * stops once one candidate runs >= 4 % below the median of those timed, never on a slow
- * straggler.  Transient memory: every candidate is
- * held until the choice (so each gets fresh pages), at most half the free device memory and at
- * most 64 GiB in total (config 2: ~2.6 GB a candidate; a 32768-codeword batch: ~21 GiB, three).
- * Results do not depend on it.
+ * straggler.  Transient memory (round 6): at most three candidates are held at a time -- the
+ * slowest is released before the next one is allocated, after a 48 MiB spacer so that the next
+ * does not get the same pages back -- so the search holds at most 3 workspaces + 48 MiB per probe
+ * beyond the third (config 2: ~2.6 GB a workspace, <= 8.9 GB held; never more than half the free
+ * device memory).  A workspace that is already big enough for B is kept as it is (placed or not):
+ * call td_reserve before the first decode to have it placed.  Results do not depend on it.
  * Occupancy: a decode of more than 512 groups of 8 codewords (B > 4096 on 256 CUs) in fp32 runs
  * three or four workgroups per CU instead of two where that finishes sooner (fp32 log-MAP 1.5x,
  * Max-Log-MAP 1.6x at B = 32768); fp64 always runs two.  Bits and Le are identical either way.
@@ -114,6 +116,10 @@ int td_decode_device(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, in
  * decoding changes the arithmetic: its gate is the BER curve, not bit-exactness.
  *   the reference GPU decoder with P sub-blocks: {6144/P, 0, 1, 1, 0.77}, TD_ALGO_MAXLOG, TD_F32
  */
+/* Debug / measurement: the windowed kernels' layout (sub-blocks per lane run of the beta kernel and
+ * of the alpha kernel, batch parts on as many streams; 0 = the layout's own choice).  Results do
+ * not depend on it; speed does.  Applies to the current and later td_set_window. */
+int td_debug_window_layout(td_handle* h, int run, int run_a, int parts);
 typedef struct td_window_params {
     int window;        /* sub-block length W (0 = exact schedule) */
     int overlap;       /* warm-up steps, 0 <= overlap <= 3*window */
@@ -121,6 +127,8 @@ typedef struct td_window_params {
     int concurrent;    /* 1: both SISOs concurrently (Jacobi) */
     double ext_scale;  /* extrinsic scale, (0, 4] */
 } td_window_params;
+/* Creates the windowed schedule's extra streams and events on the handle's device (once), so a
+ * decode after td_set_window + td_reserve allocates and creates nothing and may be captured. */
 int td_set_window(td_handle* h, const td_window_params* w);
 
 /* Kernel timing (measurement support): while enabled, hipEvents on the decode stream bracket
@@ -149,6 +157,8 @@ int td_debug_stamp_slots(void);
 int td_debug_placement(td_handle* h, float* ms, int cap, int* pick);
 /* Cost of that search: its wall time (ms) and the peak bytes of candidate workspaces it held. */
 int td_debug_placement_cost(td_handle* h, double* wall_ms, double* held_bytes);
+/* Bytes of the handle's decode workspace (0 before the first reserve / decode). */
+int td_debug_workspace_bytes(td_handle* h, unsigned long long* bytes);
 /* The placement search's stop rule on probe times ms[0..n) (host only, for tests): 1 if the search
  * would stop after them (the fast mode seen), else 0; TD_EINVAL on a bad argument. */
 int td_debug_placement_rule(const float* ms, int n);

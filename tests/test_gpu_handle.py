@@ -128,20 +128,25 @@ def test_graph_capture_windowed_two_streams():
     xs = [torch.from_numpy(np.ascontiguousarray(f)).to(dev) for f in flows]
     sb = torch.cuda.Stream(dev)
     with TurboCodec(K, f1, f2, iterations=iters) as c:
+        # the documented order: set_window (creates the streams), reserve (sizes every buffer), then
+        # capture -- no eager decode before it
         c.set_window(W, g)
         c.reserve(B)
-        eager = [c.decode(x).cpu().numpy() for x in xs]   # (the first windowed decode creates the streams)
-        torch.cuda.synchronize()
         gin = xs[0].clone()
         gout = torch.empty((B, K), dtype=torch.uint8, device=dev)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=sb):
             c.decode(gin, gout, stream=sb)
+        replayed = []
         for k in (0, 1):
             gin.copy_(xs[k])
             graph.replay()
             torch.cuda.synchronize()
-            assert np.array_equal(gout.cpu().numpy(), eager[k]), k
+            replayed.append(gout.cpu().numpy().copy())
+        eager = [c.decode(x).cpu().numpy() for x in xs]
+        torch.cuda.synchronize()
+        for k in (0, 1):
+            assert np.array_equal(replayed[k], eager[k]), k
     for k in (0, 1):
         for b in (3, 64 * 64 + 9, B - 1):
             ob, _ = O.turbo_decode_window(flows[k][b], K, f1, f2, iters, W, g)

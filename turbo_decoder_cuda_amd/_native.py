@@ -22,7 +22,8 @@ EXPORTS = (
     "td_trellis_tables", "td_qpp_table", "td_profile_enable", "td_profile_read", "td_debug_set_stamps",
     "td_debug_stamp_slots", "td_synth_seed", "td_synth_frames", "td_count_errors", "td_rand_window", "td_synth_seek",
     "td_set_window", "td_synth_modulation", "td_modulate", "td_demodulate", "td_debug_placement",
-    "td_debug_placement_rule", "td_clock_read", "td_window_steps", "td_debug_placement_cost",
+    "td_debug_placement_rule", "td_clock_read", "td_window_steps", "td_debug_placement_cost", "td_debug_window_layout",
+    "td_debug_workspace_bytes",
 )
 
 

@@ -75,7 +75,6 @@ struct td_handle {
     int place_pick = -1;
     double place_wall_ms = 0, place_held = 0;   // the search's wall time and peak bytes held
     size_t ws_bytes = 0;
-    int ws_groups = 0;
     size_t elem = 8;
     void* stamps = nullptr;     // td_debug_set_stamps
     bool prof = false;          // td_profile_enable
@@ -94,6 +93,7 @@ struct td_handle {
     int occ3 = 1;                                // TD_OCC3=0: never three workgroups per CU
     // decoding schedule (td_set_window): window 0 = exact full trellis
     td::WindowParams wp{0, 0, 0, 0, 1.0, 0};
+    int win_run = 0, win_run_a = 0, win_parts = 0;   // td_debug_window_layout (tests, measurements)
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
     td::WindowStreams wstr{};                    // the windowed schedule's extra streams (batch parts)
@@ -209,8 +209,7 @@ Carve carve_for(const td_handle* h, int G) { return carve(G, h->p.K, h->elem, h-
 hipError_t ws_malloc(void** p, size_t size) { return hipMalloc(p, size); }
 hipError_t ws_release(void* p) { return hipFree(p); }
 
-// the workspace for G groups in the handle's current layout (grown, never shrunk; ws_groups = the
-// exact-schedule groups it was placed for by td_reserve's search, 0 after a plain growth)
+// the workspace for G groups in the handle's current layout (grown, never shrunk)
 int ensure_ws(td_handle* h, int G)
 {
     const Carve c = carve_for(h, G);
@@ -219,14 +218,13 @@ int ensure_ws(td_handle* h, int G)
         TD_HIP(hipDeviceSynchronize());
         TD_HIP(ws_release(h->d_ws));
         h->d_ws = nullptr;
-        h->ws_groups = 0;
+        h->ws_bytes = 0;
     }
     if (ws_malloc(&h->d_ws, c.total) != hipSuccess) {
         h->d_ws = nullptr;
         return fail(TD_ENOMEM, "hipMalloc of the decode workspace failed (" + std::to_string(c.total) + " B)");
     }
     h->ws_bytes = c.total;
-    h->ws_groups = 0;
     return TD_OK;
 }
 
@@ -239,9 +237,8 @@ int ensure_ws(td_handle* h, int G)
 // candidates, all held until the choice (so each one gets fresh pages), times one turbo iteration
 // on each (best of two launches; zeroed workspace, results discarded; 2.20 vs 2.32 ms in the two modes at config 2) and
 // keeps the fastest.  It stops once the fast mode has been seen (placement_fast_seen below), at
-// TD_PLACEMENT_TRIALS candidates (environment, default 24; 1 = a plain allocation), or when the
-// next one would take the held candidates past the hold cap (kPlaceHoldBytes, half the free
-// device memory).  Results never depend on the placement.
+// TD_PLACEMENT_TRIALS candidates (environment, default 24; 1 = a plain allocation), holding at most
+// kPlaceLive of them at a time (below).  Results never depend on the placement.
 template <typename T>
 float probe_ws(const td_handle* h, char* ws, int G, hipStream_t st, hipEvent_t e0, hipEvent_t e1, int warm)
 {
@@ -315,35 +312,50 @@ bool placement_fast_seen(const std::vector<float>& ms)
     return slower >= 3;
 }
 
-// Candidate workspaces the search may hold at once: half the free device memory, and at most
-// kPlaceHoldBytes in total, so that a reserve never starves other handles or processes.  Round 5: 64
-// GiB (was 144): config 2 (2.6 GB a workspace) still probes up to 24 candidates,
-// config 4's 32768-codeword shard (21 GiB without the round-4 tempmax region) three instead of
-// seven.  The search's wall time and peak bytes held are recorded (td_debug_placement_cost).
-constexpr size_t kPlaceHoldBytes = (size_t)64 << 30;
+// What the search may hold at once (round 6, VERDICT round 5: rounds 3-5 held every candidate until
+// the choice, up to 64 GiB at config 2 for a 2.6 GB workspace).  At most kPlaceLive candidates are
+// live: once that many are held and the fast mode has not been seen, the slowest is released before
+// the next is allocated, and a spacer of kPlaceSpacerBytes is taken first so that the next candidate
+// does not get the released pages back in the same order.  Peak hold: kPlaceLive workspaces plus the
+// spacers (< 0.5 workspace at config 2), at most half the free device memory.  The kept candidate is
+// always live (only the slowest is released).  The search's wall time and peak bytes held are
+// recorded (td_debug_placement_cost).
+#ifndef TD_PLACE_LIVE
+#define TD_PLACE_LIVE 3
+#endif
+#ifndef TD_PLACE_SPACER_MIB
+#define TD_PLACE_SPACER_MIB 48
+#endif
+constexpr int kPlaceLive = TD_PLACE_LIVE;
+constexpr size_t kPlaceSpacerBytes = (size_t)TD_PLACE_SPACER_MIB << 20;
 
 int place_ws(td_handle* h, int G)
 {
     int trials = TD_PLACEMENT_DEFAULT;
     if (const char* e = std::getenv("TD_PLACEMENT_TRIALS")) trials = std::atoi(e);
-    if (G <= h->ws_groups || trials <= 1 || h->wp.window || 8 * G < 1024) return ensure_ws(h, G);
+    const Carve c = carve_for(h, G);
+    // a workspace that is big enough is kept as it is, placed or not (a reserve
+    // after a decode that grew it must not free it and search again)
+    if (h->d_ws && c.total <= h->ws_bytes) return TD_OK;
+    if (trials <= 1 || h->wp.window || 8 * G < 1024) return ensure_ws(h, G);
     if (h->d_ws) {
         TD_HIP(hipDeviceSynchronize());
         TD_HIP(ws_release(h->d_ws));
         h->d_ws = nullptr;
-        h->ws_groups = 0;
+        h->ws_bytes = 0;
     }
-    const Carve c = carve_for(h, G);
     // every HIP object of the search is released on every exit path, error returns included
     struct Search {
         hipStream_t st = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        std::vector<std::pair<float, void*>> cand;
+        std::vector<std::pair<float, void*>> cand;   // live candidates
+        std::vector<void*> spacers;
         ~Search()
         {
             if (st) (void)hipStreamSynchronize(st);
             for (auto& x : cand)
                 if (x.second) (void)ws_release(x.second);
+            for (void* p : spacers) (void)hipFree(p);
             if (e0) (void)hipEventDestroy(e0);
             if (e1) (void)hipEventDestroy(e1);
             if (st) (void)hipStreamDestroy(st);
@@ -355,12 +367,29 @@ int place_ws(td_handle* h, int G)
     TD_HIP(hipEventCreate(&s.e1));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const size_t hold = std::min(free_b / 2, kPlaceHoldBytes);
+    const size_t live_max = std::max<size_t>(1, std::min<size_t>(kPlaceLive, free_b / 2 / std::max<size_t>(c.total, 1)));
     std::vector<float> ms_all;
+    size_t held = 0, peak = 0;
     for (int i = 0; i < trials; ++i) {
-        if (i > 0 && (size_t)(i + 1) * c.total > hold) break;   // memory guard
+        if (s.cand.size() >= live_max) {
+            if (live_max < 2) break;   // no room to compare
+            size_t worst = 0;
+            for (size_t k = 1; k < s.cand.size(); ++k)
+                if (s.cand[k].first > s.cand[worst].first) worst = k;
+            TD_HIP(hipStreamSynchronize(s.st));
+            (void)ws_release(s.cand[worst].second);
+            s.cand.erase(s.cand.begin() + (long)worst);
+            held -= c.total;
+            void* sp = nullptr;
+            if (kPlaceSpacerBytes && hipMalloc(&sp, kPlaceSpacerBytes) == hipSuccess) {
+                s.spacers.push_back(sp);
+                held += kPlaceSpacerBytes;
+            }
+        }
         void* p = nullptr;
         if (ws_malloc(&p, c.total) != hipSuccess) break;   // out of memory: choose among those we have
+        held += c.total;
+        peak = std::max(peak, held);
         s.cand.emplace_back(1e30f, p);
         const int warm = i == 0 ? 4 : 1;
         const float ms = h->elem == 8 ? probe_ws<double>(h, static_cast<char*>(p), G, s.st, s.e0, s.e1, warm)
@@ -375,13 +404,17 @@ int place_ws(td_handle* h, int G)
     for (size_t i = 1; i < s.cand.size(); ++i)
         if (s.cand[i].first < s.cand[best].first) best = i;
     h->place_ms = ms_all;
-    h->place_pick = (int)best;
-    h->place_held = (double)s.cand.size() * (double)c.total;
+    h->place_pick = -1;   // index into ms_all of the kept candidate
+    for (size_t i = 0; i < ms_all.size(); ++i)
+        if (ms_all[i] == s.cand[best].first) {
+            h->place_pick = (int)i;
+            break;
+        }
+    h->place_held = (double)peak;
     h->place_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     h->d_ws = s.cand[best].second;
-    s.cand[best].second = nullptr;   // kept; the guard frees the others
+    s.cand[best].second = nullptr;   // kept; the guard frees the others and the spacers
     h->ws_bytes = c.total;
-    h->ws_groups = G;
     return TD_OK;
 }
 
@@ -446,6 +479,38 @@ int window_bufs(td_handle* h, const td::DecodeParams<T>& dp, td::WindowBufs<T>& 
     return TD_OK;
 }
 
+// The windowed schedule's extra streams and their fork / join events (its batch parts 1..; part 0
+// runs on the caller's stream), made by td_set_window on the handle's device -- never inside a
+// decode, which may be under stream capture.  All or nothing: a failure releases
+// whatever was made and leaves the handle without them.
+void release_wstr(td::WindowStreams& w)
+{
+    for (int i = 1; i < td::kSwMaxParts; ++i) {
+        if (w.st[i]) (void)hipStreamDestroy(w.st[i]);
+        if (w.fork[i]) (void)hipEventDestroy(w.fork[i]);
+        if (w.join[i]) (void)hipEventDestroy(w.join[i]);
+    }
+    w = td::WindowStreams{};
+}
+
+int ensure_wstr(td_handle* h)
+{
+    if (h->wstr.st[1]) return TD_OK;
+    td::WindowStreams w{};
+    hipError_t e = hipSuccess;
+    for (int i = 1; i < td::kSwMaxParts && e == hipSuccess; ++i) {
+        e = hipStreamCreateWithFlags(&w.st[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&w.fork[i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&w.join[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        release_wstr(w);
+        return hip_fail(e, "td_set_window: stream / event creation");
+    }
+    h->wstr = w;
+    return TD_OK;
+}
+
 template <typename T>
 int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int all_iters, void* d_le,
                     hipStream_t st)
@@ -482,6 +547,7 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
     dp.sys2_in_turbo = (TD_SYS2_IN_TURBO && !h->wp.window) ? 1 : 0;
     td::WindowBufs<T> wb{};
     if (h->wp.window) {   // sized before anything is enqueued (a growth synchronises the device)
+        if (!h->wstr.st[1]) return fail(TD_EINVAL, "td_decode_device: the windowed schedule's streams are missing");
         rc = window_bufs<T>(h, dp, wb);
         if (rc) return rc;
     }
@@ -510,16 +576,8 @@ int decode_device_t(td_handle* h, const void* d_llr, int B, uint8_t* d_bits, int
                                 : td::launch_demux<T>(dp, static_cast<const T*>(d_llr), st);
     if (e != hipSuccess) return hip_fail(e, "launch_demux");
     if (ev) TD_HIP(hipEventRecord(ev[1], st));
-    if (h->wp.window) {
-        if (!h->wstr.st[1]) {   // created once, on the handle's device (part 0 runs on the caller's stream)
-            for (int i = 1; i < td::kSwMaxParts; ++i) {
-                TD_HIP(hipStreamCreateWithFlags(&h->wstr.st[i], hipStreamNonBlocking));
-                TD_HIP(hipEventCreateWithFlags(&h->wstr.fork[i], hipEventDisableTiming));
-                TD_HIP(hipEventCreateWithFlags(&h->wstr.join[i], hipEventDisableTiming));
-            }
-        }
-        e = td::launch_window<T>(dp, h->wp, wb, st, h->wstr);
-    }
+    if (h->wp.window)
+        e = td::launch_window<T>(dp, h->wp, wb, st, h->wstr);   // streams made by td_set_window
     else
         e = td::launch_turbo<T>(dp, st);
     if (e != hipSuccess) return hip_fail(e, h->wp.window ? "launch_window" : "launch_turbo");
@@ -729,8 +787,7 @@ int td_create(td_handle** out, const td_params* p)
     h->p = *p;
     h->elem = p->precision == TD_F64 ? sizeof(double) : sizeof(float);
     {
-        const char* rot = std::getenv("TD_ROLE_ROT");   // diagnostics: 0 disables the role rotation
-        h->role_cus = (rot && std::atoi(rot) == 0) ? 0 : prop.multiProcessorCount;
+        h->role_cus = prop.multiProcessorCount;
         const char* o3 = std::getenv("TD_OCC3");      // 0: large batches stay on two workgroups per CU
         h->occ3 = (o3 && std::atoi(o3) == 0) ? 0 : 1;
     }
@@ -806,11 +863,7 @@ int td_destroy(td_handle* h)
     if (h->d_hle) (void)hipFree(h->d_hle);
     if (h->d_win) (void)hipFree(h->d_win);
     if (h->d_wws) (void)hipFree(h->d_wws);
-    for (int i = 1; i < td::kSwMaxParts; ++i) {
-        if (h->wstr.st[i]) (void)hipStreamDestroy(h->wstr.st[i]);
-        if (h->wstr.fork[i]) (void)hipEventDestroy(h->wstr.fork[i]);
-        if (h->wstr.join[i]) (void)hipEventDestroy(h->wstr.join[i]);
-    }
+    release_wstr(h->wstr);
     for (auto& tri : h->ev)
         for (auto& e : tri) (void)hipEventDestroy(e);
     if (h->ws_free) (void)hipEventDestroy(h->ws_free);
@@ -849,13 +902,27 @@ int td_set_window(td_handle* h, const td_window_params* w)
         return fail(TD_EINVAL, "td_set_window: overlap must be in [0, 3*window]");
     if (!(w->ext_scale > 0.0) || !(w->ext_scale <= 4.0))
         return fail(TD_EINVAL, "td_set_window: ext_scale must be in (0, 4]");
-    // TD_WINDOW_RUN (environment, tests): sub-blocks per lane run, forcing the run layout on batches too
-    // small to choose it (the results do not depend on it)
-    const char* run = std::getenv("TD_WINDOW_RUN");
-    const char* run_a = std::getenv("TD_WINDOW_RUN_A");
-    const char* parts = std::getenv("TD_WINDOW_PARTS");
+    TD_HIP(hipSetDevice(h->p.device));
+    const int rc = ensure_wstr(h);
+    if (rc) return rc;
     h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale,
-                             run ? std::atoi(run) : 0, run_a ? std::atoi(run_a) : 0, parts ? std::atoi(parts) : 0};
+                             h->win_run, h->win_run_a, h->win_parts};
+    return TD_OK;
+}
+
+int td_debug_window_layout(td_handle* h, int run, int run_a, int parts)
+{
+    if (!h) return fail(TD_EINVAL, "td_debug_window_layout: null handle");
+    if (run < 0 || run_a < 0 || parts < 0 || parts > td::kSwMaxParts)
+        return fail(TD_EINVAL, "td_debug_window_layout: run, run_a >= 0 and 0 <= parts <= 4");
+    h->win_run = run;
+    h->win_run_a = run_a;
+    h->win_parts = parts;
+    if (h->wp.window) {
+        h->wp.run = run;
+        h->wp.run_a = run_a;
+        h->wp.parts = parts;
+    }
     return TD_OK;
 }
 
@@ -924,6 +991,13 @@ int td_debug_placement_cost(td_handle* h, double* wall_ms, double* held_bytes)
     if (!h) return fail(TD_EINVAL, "td_debug_placement_cost: null handle");
     if (wall_ms) *wall_ms = h->place_wall_ms;
     if (held_bytes) *held_bytes = h->place_held;
+    return TD_OK;
+}
+
+int td_debug_workspace_bytes(td_handle* h, unsigned long long* bytes)
+{
+    if (!h || !bytes) return fail(TD_EINVAL, "td_debug_workspace_bytes: null argument");
+    *bytes = (unsigned long long)h->ws_bytes;
     return TD_OK;
 }
 

@@ -2056,7 +2056,7 @@ struct WgPos {
 // dispatch round instead cost 4 % after a kernel with many small blocks had shifted the placement;
 // the pairing A/F1 + B/F0 measured 0.7 % slower, and beta beside a loader -- alpha alone on its SIMD
 // in the F pass -- 1.3 % slower).  If two waves of the workgroup share a SIMD, the wave index stands
-// in for the SIMD.  role_cus = 0 or no slot words (diagnostics, TD_ROLE_ROT=0): role = wave.
+// in for the SIMD.  role_cus = 0 or no slot words: role = wave.
 __device__ __forceinline__ WgPos wg_pos(int role_cus, unsigned* slots)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -85,6 +85,12 @@ class TurboCodec:
         N.check(N.lib().td_debug_placement_cost(self._h, C.byref(w), C.byref(b)))
         return w.value, b.value
 
+    def workspace_bytes(self) -> int:
+        """Bytes of the decode workspace (td_debug_workspace_bytes)."""
+        v = C.c_ulonglong(0)
+        N.check(N.lib().td_debug_workspace_bytes(self._h, C.byref(v)))
+        return int(v.value)
+
     def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
                    concurrent: bool = False) -> None:
         """Windowed schedule (td_set_window; BASELINE config 5); window=0: exact.
@@ -93,6 +99,11 @@ class TurboCodec:
         w = N.TdWindowParams(int(window), int(overlap), int(bool(nii)), int(bool(concurrent)), float(ext_scale))
         N.check(N.lib().td_set_window(self._h, C.byref(w)))
         self.window = int(window)
+
+    def debug_window_layout(self, run: int = 0, run_a: int = 0, parts: int = 0) -> None:
+        """Windowed kernels' layout for tests and measurements (td_debug_window_layout): sub-blocks
+        per lane run (beta and alpha kernels) and batch parts; 0 = the layout's own choice."""
+        N.check(N.lib().td_debug_window_layout(self._h, int(run), int(run_a), int(parts)))
 
     # -- TurboDecoding, host arrays ------------------------------------------------------
     def TurboDecoding(self, flow: np.ndarray, return_le: bool = False):
