@@ -140,7 +140,7 @@ N_SIMDS = 1024   # 256 CUs x 4 SIMDs (MI355X)
 WINDOW_ISSUE_CEILING = 0.754
 
 
-def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None):
+def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None, exact_table=False):
     """Roofline record of the windowed schedule (BASELINE config 5: fp64 log-MAP, window 64, overlap 30)
     from the live decode time and the committed PMC of the same kernels (profiles/traffic.json key
     K6144_B32768_it8_f64_logmap_w64g30: FETCH_SIZE x2 + WRITE_SIZE bytes and SQ_INSTS_VALU per decode,
@@ -148,7 +148,7 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None):
     4 cycles; 1024 SIMDs at the shader clock) and HBM (counter bytes against the 8 TB/s spec and the
     6.29 TB/s streaming ceiling).  The algorithmic-bytes fraction is the metric's contract, as for
     the exact kernel."""
-    rec = load_traffic_rec(f"K{K}_B{B}_it{iters}_f64_logmap_w64g30")
+    rec = load_traffic_rec(f"K{K}_B{B}_it{iters}_f64_logmap_w64g30" + ("_exacttable" if exact_table else ""))
     clk = sclk_ghz or SCLK_GHZ
     alg = B * (8 * (3 * K + 12) + K)
     out = {"kernels": "sw_demux_kernel + (sw_alpha_kernel + sw_beta_kernel) x 2 SISOs x iterations + bits_transpose",
@@ -173,11 +173,11 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None):
         floor = max(out["valu_floor_ms"], out["hbm_floor_ms"])
         out.update({"binding": "valu" if out["valu_floor_ms"] >= out["hbm_floor_ms"] else "hbm",
                     "frac_of_binding": round(floor / decode_ms, 4),
-                    # the same VALU fraction against the issue rate the kernels' instruction mix reaches
-                    # at their occupancy in the microbenchmark (a measured ceiling, not a spec)
-                    "valu_issue_ceiling": WINDOW_ISSUE_CEILING,
-                    "valu_issue_ceiling_source": "scripts/ubench_window.hip, 2 waves/SIMD (profiles/r05/ubench_window.jsonl)",
-                    "frac_of_issue_ceiling": round(out["valu_issue_frac"] / WINDOW_ISSUE_CEILING, 4)})
+                    "lane_valu_per_position": round(vi * 64 / (B * 2 * iters * (K + 3)), 1)})
+        if exact_table:   # the issue rate the exact-table mix reaches in the microbenchmark (a measured ceiling)
+            out.update({"valu_issue_ceiling": WINDOW_ISSUE_CEILING,
+                        "valu_issue_ceiling_source": "scripts/ubench_window.hip, 2 waves/SIMD (profiles/r05/ubench_window.jsonl)",
+                        "frac_of_issue_ceiling": round(out["valu_issue_frac"] / WINDOW_ISSUE_CEILING, 4)})
     return out
 
 
@@ -783,11 +783,12 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
 
     res = {}
     cases = [(p, g, 0, False) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f64", "maxlog"), ("f32", "maxlog"))]
-    cases += [(p, g, 64, True) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
+    cases += [(p, g, 64, True) for p, g in (("f64", "logmap"), ("f64", "logmap-exact"), ("f32", "logmap"), ("f32", "maxlog"))]
     if a.batch != CONFIG5_BATCH:
         cases += [(p, g, 0, True) for p, g in (("f64", "logmap"), ("f32", "logmap"), ("f32", "maxlog"))]
     big = None
-    for prec, algo, win, on_big in cases:
+    for prec, algo_form, win, on_big in cases:
+        algo, exact_table = algo_form.split("-")[0], algo_form.endswith("-exact")
         if prec == a.precision and algo == a.algo and win == a.window and not on_big:
             continue
         if on_big:
@@ -802,6 +803,7 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         x = xb if prec == "f64" else xb.float()
         c = TurboCodec(a.K, f1, f2, iterations=a.iters, algo=algo, precision=prec, device=dev.index)
         if win:
+            c.set_window_maxstar(exact_table)
             c.set_window(win, a.overlap)
         c.reserve(B)
         b = torch.empty((B, a.K), dtype=torch.uint8, device=dev)
@@ -828,7 +830,8 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         c.close()
         errs = int((b != ub).sum().item())
         del x
-        key = f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else (f"_B{B}" if on_big else ""))
+        key = f"{prec}_{algo}" + (f"_window{win}_overlap{a.overlap}" if win else (f"_B{B}" if on_big else "")) + \
+            ("_exact_table" if exact_table else "")
         cfg = "5" if win else ("4 (one GPU's shard)" if on_big and prec == "f64" and algo == "logmap"
                                else ("3" if algo == "maxlog" and prec == "f64" else None))
         res[key] = {"value": round(B * a.K * steps / dt / 1e6, 3), "unit": "Mbit/s", "batch": B, "config": cfg,
@@ -836,7 +839,11 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
         if win and prec == "f64" and algo == "logmap":
             mean_ghz = (prec_pw["sclk_mhz_mean"] / 1e3) if prec_pw and prec_pw.get("sclk_mhz_mean") else None
             res[key]["roofline"] = window_roofline(a.K, B, a.iters, dt / steps * 1e3, mean_ghz or vclk,
-                                                   "amdsmi mean over the timed region" if mean_ghz else None)
+                                                   "amdsmi mean over the timed region" if mean_ghz else None,
+                                                   exact_table)
+            res[key]["maxstar"] = ("log_map.cpp's E_algorithm (exact three-read table)" if exact_table else
+                                   "one-read table: E_algorithm's correction at the midpoint of d's bucket, 8 an octave "
+                                   "(td_set_window_maxstar; BER curve in DESIGN.md 8.3)")
             res[key]["roofline"]["sclk_td_clock_read_ghz"] = round(vclk, 4) if vclk else None
             res[key]["power"] = prec_pw
     if big is not None and a.K == 6144:

@@ -127,6 +127,15 @@ typedef struct td_window_params {
     int concurrent;    /* 1: both SISOs concurrently (Jacobi) */
     double ext_scale;  /* extrinsic scale, (0, 4] */
 } td_window_params;
+/* The max* of the windowed log-MAP schedule (round 6).  TD_WMAXSTAR_FAST (the default): the
+ * reference's 16-step correction (log_map.cpp:14-18, 779-801) on a finer bucket grid (8 buckets an
+ * octave of d, each with the reference's value at its midpoint), read with ONE table read and no
+ * threshold compare -- it differs from E_algorithm only for d within half a bucket of one of its
+ * thresholds, by one table step; TD_WMAXSTAR_EXACT: E_algorithm exactly (the exact schedule's
+ * form).  The windowed schedule is BER-gated either way (the BER curves of both).
+ * No effect on the exact schedule or Max-Log-MAP. */
+enum td_window_maxstar { TD_WMAXSTAR_FAST = 0, TD_WMAXSTAR_EXACT = 1 };
+int td_set_window_maxstar(td_handle* h, int form);
 /* Creates the windowed schedule's extra streams and events on the handle's device (once), so a
  * decode after td_set_window + td_reserve allocates and creates nothing and may be captured. */
 int td_set_window(td_handle* h, const td_window_params* w);
@@ -230,8 +239,10 @@ int td_abi_version(void);
 /*
  * Host evaluation of the exact bucket form of E_algorithm used on the device (no GPU needed):
  * max(x,y) + table(|y-x|) through the 29-bucket LUT the kernels read from LDS.  Lets CPU
- * tests prove LUT == log_map.cpp:779-801 for every threshold.  algo = enum td_algo.
+ * tests prove LUT == log_map.cpp:779-801 for every threshold.  algo = enum td_algo, or
+ * TD_MAXSTAR_WINDOW_FAST: the windowed schedule's one-read table (td_set_window_maxstar).
  */
+#define TD_MAXSTAR_WINDOW_FAST 2
 double td_maxstar_host_f64(double x, double y, int algo);
 float td_maxstar_host_f32(float x, float y, int algo);
 

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 ALGO_LOGMAP = 0
 ALGO_MAXLOG = 1
+ALGO_LOGMAP_Q = 2   # the windowed schedule's one-read max* table (td_set_window_maxstar TD_WMAXSTAR_FAST)
 
 
 def build(force: bool = False) -> str:
@@ -57,6 +58,10 @@ def lib():
         L.tdo_maxstar.restype = C.c_double
         L.tdo_maxstar_f32.argtypes = [C.c_float, C.c_float]
         L.tdo_maxstar_f32.restype = C.c_float
+        L.tdo_maxstar_q.argtypes = [C.c_double, C.c_double]
+        L.tdo_maxstar_q.restype = C.c_double
+        L.tdo_maxstar_q_f32.argtypes = [C.c_float, C.c_float]
+        L.tdo_maxstar_q_f32.restype = C.c_float
         L.tdo_maxstar_seq.argtypes = [P, C.c_int]
         L.tdo_maxstar_seq.restype = C.c_double
         L.tdo_demultiplex.argtypes = [P, C.c_int, P, P]
@@ -115,6 +120,14 @@ def maxstar(x: float, y: float) -> float:
 
 def maxstar_f32(x: float, y: float) -> float:
     return lib().tdo_maxstar_f32(x, y)
+
+
+def maxstar_q(x: float, y: float) -> float:
+    return lib().tdo_maxstar_q(x, y)
+
+
+def maxstar_q_f32(x: float, y: float) -> float:
+    return lib().tdo_maxstar_q_f32(x, y)
 
 
 def siso(recs: np.ndarray, La: np.ndarray, terminated: int = 1, algo: int = ALGO_LOGMAP) -> np.ndarray:

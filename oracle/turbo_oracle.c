@@ -56,6 +56,48 @@ float tdo_maxstar_f32(float x, float y)
     return (x > y ? x : y) + temp;
 }
 
+/* The windowed schedule's one-read max* (TDO_ALGO_LOGMAP_Q; not the reference's -- the sub-block
+ * schedule is BER-gated).  The buckets of d = |y - x|: exponent + 3 mantissa bits (8 an octave); row 0
+ * holds every d below 2^-4 * 9/8, row 56 every d >= 8; rows 1..55 are [2^e (1 + m/8), 2^e (1 + (m+1)/8))
+ * with e = q/8 - 4, m = q % 8.  A row's correction is E_algorithm's (above) at the row's midpoint, 0 in
+ * row 56.  The row comes from the bits of d exactly as the kernels take it (sign outside the field). */
+#define TDO_QBITS 3
+#define TDO_QROWS ((7 << TDO_QBITS) + 1)
+static double q_correction(int q)
+{
+    if (q >= TDO_QROWS - 1) return 0.0;
+    const int e = q >> TDO_QBITS, m = q & ((1 << TDO_QBITS) - 1);
+    const double lo = ldexp(1.0 + (double)m / (1 << TDO_QBITS), e - 4);
+    const double hi = ldexp(1.0 + (double)(m + 1) / (1 << TDO_QBITS), e - 4);
+    const double mid = 0.5 * (lo + hi);
+    if (mid >= 4.3758) return 0.0;
+    int i;
+    for (i = 0; i < 16 && mid >= k_idx[i]; i++) {
+    }
+    return k_tab[i - 1];
+}
+static int q_row(uint32_t hi, int shift, int width, int base)
+{
+    int q = (int)((hi >> shift) & ((1u << width) - 1)) - base;
+    return q < 0 ? 0 : (q > TDO_QROWS - 1 ? TDO_QROWS - 1 : q);
+}
+double tdo_maxstar_q(double x, double y)
+{
+    const double d = y - x;
+    uint64_t b;
+    memcpy(&b, &d, sizeof b);
+    const int q = q_row((uint32_t)(b >> 32), 20 - TDO_QBITS, 11 + TDO_QBITS, (1023 - 4) << TDO_QBITS);
+    return (x > y ? x : y) + q_correction(q);
+}
+float tdo_maxstar_q_f32(float x, float y)
+{
+    const float d = y - x;
+    uint32_t b;
+    memcpy(&b, &d, sizeof b);
+    const int q = q_row(b, 23 - TDO_QBITS, 8 + TDO_QBITS, (127 - 4) << TDO_QBITS);
+    return (x > y ? x : y) + (float)q_correction(q);
+}
+
 /* ---------------------------------------------------------------- code tables */
 
 /* gen_g_matrix, log_map.cpp:114-169: octal generator -> 4 binary taps, MSB first */
@@ -379,20 +421,24 @@ void tdo_demultiplex(const double* flow, int K, const int* pi, double* yk) { dem
 #define REAL double
 #define SFX f64
 #define MAXSTAR(x, y) tdo_maxstar((x), (y))
+#define MAXSTAR_Q(x, y) tdo_maxstar_q((x), (y))
 #include "turbo_oracle_siso.inc"
 #include "turbo_oracle_window.inc"
 #undef REAL
 #undef SFX
 #undef MAXSTAR
+#undef MAXSTAR_Q
 
 #define REAL float
 #define SFX f32
 #define MAXSTAR(x, y) tdo_maxstar_f32((x), (y))
+#define MAXSTAR_Q(x, y) tdo_maxstar_q_f32((x), (y))
 #include "turbo_oracle_siso.inc"
 #include "turbo_oracle_window.inc"
 #undef REAL
 #undef SFX
 #undef MAXSTAR
+#undef MAXSTAR_Q
 
 /* ---------------------------------------------------------------- batch + threads */
 typedef struct {

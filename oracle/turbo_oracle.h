@@ -33,6 +33,8 @@ extern "C" {
 /* algorithm selector */
 #define TDO_ALGO_LOGMAP 0    /* table Jacobian max*  (TYPE_DECODER 1, log_map.h:26) */
 #define TDO_ALGO_MAXLOG 1    /* max* == max          (TYPE_DECODER 2, log_map.h:27; not implemented in the ref) */
+#define TDO_ALGO_LOGMAP_Q 2  /* the windowed schedule's one-read table (td_set_window_maxstar TD_WMAXSTAR_FAST):
+                                E_algorithm's correction at the midpoint of d's bucket, 8 buckets an octave */
 
 /* Trellis tables, same meaning as TURBO_TRELLIS (log_map.h:58-66). */
 typedef struct {
@@ -83,6 +85,9 @@ double tdo_maxstar(double x, double y);
 /* left fold, log_map.cpp:817-829 */
 double tdo_maxstar_seq(const double* v, int n);
 float tdo_maxstar_f32(float x, float y);
+/* TDO_ALGO_LOGMAP_Q's max* (restated from its definition: DESIGN.md 8.3, td_tables.h build_qlut) */
+double tdo_maxstar_q(double x, double y);
+float tdo_maxstar_q_f32(float x, float y);
 
 /* log_map.cpp:1083-1127: flow (already scaled by 0.5) -> yk[4L] */
 void tdo_demultiplex(const double* flow, int K, const int* pi, double* yk);

@@ -3,7 +3,9 @@
 Paired Monte-Carlo on the GPU: at every Eb/N0 point the SAME frames of main.cpp's stream
 (srand(seed + point), the device generator, bit-identical to the reference's frames) go through
 the exact schedule (log_map.cpp's arithmetic, bit-exact against the compiled reference) and
-through the windowed schedule (td_set_window), both fp64 table log-MAP, K=6144, 8 iterations.
+through the windowed schedule (td_set_window) with each max* form (td_set_window_maxstar: the
+one-read table "window" and log_map.cpp's E_algorithm "window_exact_table"), all fp64 log-MAP,
+K=6144, 8 iterations.
 A fixed frame count per point (no early stop) keeps the two sides on identical inputs, so the
 difference in bit and block errors is the schedule's alone.  Writes one JSON record with the
 per-point counts and the Eb/N0 where each curve crosses BER 1e-3 and 1e-4 (log-linear
@@ -65,19 +67,23 @@ def main(argv=None):
     rec = {"K": a.K, "iters": a.iters, "window": a.window, "overlap": a.overlap, "nii": a.nii,
            "algo": "logmap", "precision": "f64", "frames_per_point": a.frames, "seed": a.seed, "points": []}
     t0 = time.time()
+    names = ("exact", "window", "window_exact_table")
     with TurboCodec(a.K, a.f1, a.f2, iterations=a.iters) as ex, \
-            TurboCodec(a.K, a.f1, a.f2, iterations=a.iters) as win:
+            TurboCodec(a.K, a.f1, a.f2, iterations=a.iters) as win, \
+            TurboCodec(a.K, a.f1, a.f2, iterations=a.iters) as winx:
         win.set_window(a.window, a.overlap, nii=a.nii)
+        winx.set_window_maxstar(True)
+        winx.set_window(a.window, a.overlap, nii=a.nii)
         for pi, e in enumerate(a.ebn0):
             ex.synth_seed(a.seed + pi)
-            cnt = {s: {"bit": [0] * a.iters, "block": [0] * a.iters} for s in ("exact", "window")}
+            cnt = {s: {"bit": [0] * a.iters, "block": [0] * a.iters} for s in names}
             differ = 0
             done = 0
             while done < a.frames:
                 b = min(B, a.frames - done)
                 ex.synth(b, e, info[:b], llr[:b])
                 per = {}
-                for name, c in (("exact", ex), ("window", win)):
+                for name, c in zip(names, (ex, win, winx)):
                     c.decode(llr[:b], bits[:b], all_iters=True)
                     err = c.count_errors(bits[:b], info[:b]).cpu()
                     per[name] = err[:, -1].clone()
@@ -87,25 +93,24 @@ def main(argv=None):
                 differ += int(((per["exact"] != 0) != (per["window"] != 0)).sum())
                 done += b
             bits_total = a.frames * a.K
-            pt = {"ebn0_db": e, "frames": a.frames,
-                  "exact": cnt["exact"], "window": cnt["window"],
-                  "ber_exact": cnt["exact"]["bit"][-1] / bits_total,
-                  "ber_window": cnt["window"]["bit"][-1] / bits_total,
-                  "bler_exact": cnt["exact"]["block"][-1] / a.frames,
-                  "bler_window": cnt["window"]["block"][-1] / a.frames,
-                  "frames_error_state_differs": differ}
+            pt = {"ebn0_db": e, "frames": a.frames, "frames_error_state_differs": differ}
+            for n_ in names:
+                pt[n_] = cnt[n_]
+                pt[f"ber_{n_}"] = cnt[n_]["bit"][-1] / bits_total
+                pt[f"bler_{n_}"] = cnt[n_]["block"][-1] / a.frames
             rec["points"].append(pt)
-            print(f"Eb/N0 {e:.3f}: BER exact {pt['ber_exact']:.3e} window {pt['ber_window']:.3e}  "
-                  f"bits {cnt['exact']['bit'][-1]} / {cnt['window']['bit'][-1]}  "
-                  f"blocks {cnt['exact']['block'][-1]} / {cnt['window']['block'][-1]}  "
-                  f"({time.time() - t0:.0f} s)", flush=True)
+            print(f"Eb/N0 {e:.3f}: BER " + "  ".join(f"{n_} {pt['ber_' + n_]:.3e}" for n_ in names) +
+                  "  bits " + " / ".join(str(cnt[n_]["bit"][-1]) for n_ in names) +
+                  "  blocks " + " / ".join(str(cnt[n_]["block"][-1]) for n_ in names) +
+                  f"  ({time.time() - t0:.0f} s)", flush=True)
     eb = [p["ebn0_db"] for p in rec["points"]]
     for tgt in (1e-3, 1e-4, 1e-5):
-        ce = crossing(eb, [p["ber_exact"] for p in rec["points"]], tgt)
-        cw = crossing(eb, [p["ber_window"] for p in rec["points"]], tgt)
-        rec[f"crossing_{tgt:.0e}"] = {"exact_db": ce, "window_db": cw,
-                                      "delta_db": (cw - ce) if ce is not None and cw is not None else None}
-        print(f"BER {tgt:.0e}: exact {ce} dB, window {cw} dB", flush=True)
+        cr = {n_: crossing(eb, [p["ber_" + n_] for p in rec["points"]], tgt) for n_ in names}
+        r = {f"{n_}_db": cr[n_] for n_ in names}
+        for n_ in names[1:]:
+            r[f"delta_{n_}_db"] = (cr[n_] - cr["exact"]) if cr[n_] is not None and cr["exact"] is not None else None
+        rec[f"crossing_{tgt:.0e}"] = r
+        print(f"BER {tgt:.0e}: " + ", ".join(f"{n_} {cr[n_]} dB" for n_ in names), flush=True)
     rec["wall_s"] = round(time.time() - t0, 1)
     if a.out:
         with open(a.out, "w") as f:

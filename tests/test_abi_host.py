@@ -96,6 +96,44 @@ def test_maxstar_lut_random_and_edges():
         assert g(x, y, N.TD_ALGO_LOGMAP) == np.float32(O.maxstar_f32(float(x), float(y)))
 
 
+def test_window_one_read_maxstar():
+    """The windowed schedule's one-read max* (td_set_window_maxstar TD_WMAXSTAR_FAST, td_tables.h
+    build_qlut): the library's host evaluation equals the C restatement (TDO_ALGO_LOGMAP_Q, restated
+    from the definition) on random pairs, every bucket edge of the 8-an-octave grid and the
+    reference's thresholds, in fp64 and fp32; and it equals E_algorithm (log_map.cpp:779-801) except
+    where |y - x| lies in a bucket that holds one of the reference's thresholds, where the two differ
+    by exactly one table step."""
+    f = N.lib().td_maxstar_host_f64
+    g = N.lib().td_maxstar_host_f32
+    rng = np.random.default_rng(7)
+    xs = rng.normal(0, 3, 20000)
+    ys = xs + rng.exponential(1.5, 20000) * rng.choice([-1, 1], 20000)
+    grid = [np.ldexp(1 + m / 8, e) for e in range(-6, 5) for m in range(8)]
+    idx = [0.08824, 0.19587, 0.31026, 0.43275, 0.56508, 0.70963, 0.86972,
+           1.0502, 1.2587, 1.5078, 1.8212, 2.2522, 2.9706, 3.6764, 4.3758]
+    edges = [v for t in grid + idx for v in (np.nextafter(t, -1), t, np.nextafter(t, 99))] + [0.0, 1e-300, 7.99, 8.0, 1e6]
+    xs = np.concatenate([xs, np.full(len(edges), 2.25), np.full(len(edges), -7.0)])
+    ys = np.concatenate([ys, 2.25 - np.array(edges), -7.0 + np.array(edges)])
+    # the buckets (of the 8-an-octave grid) that hold a reference threshold
+    def bucket(d):   # octave e, eighth m of it: [2^e (1 + m/8), 2^e (1 + (m+1)/8))
+        if d <= 0:
+            return -10**9
+        m, e = np.frexp(d)   # d = m 2^e, m in [0.5, 1)
+        return (int(e) - 1) * 8 + int((2 * m - 1) * 8)
+    mixed = {bucket(t) for t in idx}
+    tab = [0.69315, 0.65, 0.6, 0.55, 0.5, 0.45, 0.4, 0.35, 0.3, 0.25, 0.2, 0.15, 0.1, 0.05, 0.025, 0.0125]
+    steps = {round(abs(a - b), 12) for a, b in zip(tab, tab[1:] + [0.0])}
+    for x, y in zip(xs, ys):
+        q = f(x, y, N.TD_MAXSTAR_WINDOW_FAST)
+        assert q == O.maxstar_q(x, y), (x, y)
+        d = abs(y - x)
+        if q != O.maxstar(x, y):
+            assert bucket(d) in mixed, (x, y, d)
+            assert round(abs(q - O.maxstar(x, y)), 12) in steps, (x, y)
+    for x, y in zip(xs[:4000].astype(np.float32), ys[:4000].astype(np.float32)):
+        assert g(x, y, N.TD_MAXSTAR_WINDOW_FAST) == np.float32(O.maxstar_q_f32(float(x), float(y)))
+
+
 def test_create_rejects_bad_arguments():
     L = N.lib()
     h = C.c_void_p()

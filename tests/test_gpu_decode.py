@@ -321,8 +321,9 @@ def test_compat_turbo_decoding(driver, tmp_path, name):
     assert np.array_equal(flow2, d["flow"] * 0.5)
 
 
-@pytest.mark.parametrize("algo,W,g", [("maxlog", 16, 48), ("logmap", 64, 30), ("logmap", 32, 30)])
-def test_compat_window_schedule(driver, tmp_path, algo, W, g):
+@pytest.mark.parametrize("algo,W,g,table", [("maxlog", 16, 48, ""), ("logmap", 64, 30, ""), ("logmap", 32, 30, ""),
+                                            ("logmap", 64, 30, "exact")])
+def test_compat_window_schedule(driver, tmp_path, algo, W, g, table):
     """The compat layer's opt-in sub-block schedule (TD_WINDOW / TD_OVERLAP, read at
     TurboCodingInit): the unchanged caller's TurboDecoding then runs the windowed kernels.  Its rows
     equal the windowed restatement (oracle/turbo_oracle_window.inc) bit for bit; with Max-Log-MAP
@@ -332,11 +333,12 @@ def test_compat_window_schedule(driver, tmp_path, algo, W, g):
     K, f1, f2, nf, it = (40, 3, 10, 4, 4) if algo == "maxlog" else (1024, 31, 64, 3, 4)
     _, flow = O.synth_batch(K, f1, f2, 0.3, 51 + W, nf)
     flow.astype(np.float64).tofile(tmp_path / "flow.bin")
-    env = dict(os.environ, TD_ITERATIONS=str(it), TD_WINDOW=str(W), TD_OVERLAP=str(g), TD_ALGO=algo)
+    env = dict(os.environ, TD_ITERATIONS=str(it), TD_WINDOW=str(W), TD_OVERLAP=str(g), TD_ALGO=algo,
+               TD_WINDOW_MAXSTAR=table)
     subprocess.run([driver, "decode", str(K), str(f1), str(f2), str(nf), str(tmp_path / "flow.bin"),
                     str(tmp_path / "out.bin")], env=env, timeout=300, check=True)
     out = np.fromfile(tmp_path / "out.bin", dtype=np.int32).reshape(nf, 15, K)[:, :it].astype(np.uint8)
-    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else (O.ALGO_LOGMAP if table == "exact" else O.ALGO_LOGMAP_Q)
     for b in range(nf):
         wb, _ = O.turbo_decode_window(flow[b], K, f1, f2, it, W, g, algo=oalgo)
         assert np.array_equal(out[b], wb), f"frame {b}"

@@ -149,5 +149,5 @@ def test_graph_capture_windowed_two_streams():
             assert np.array_equal(replayed[k], eager[k]), k
     for k in (0, 1):
         for b in (3, 64 * 64 + 9, B - 1):
-            ob, _ = O.turbo_decode_window(flows[k][b], K, f1, f2, iters, W, g)
+            ob, _ = O.turbo_decode_window(flows[k][b], K, f1, f2, iters, W, g, algo=O.ALGO_LOGMAP_Q)
             assert np.array_equal(eager[k][b], ob[-1]), (k, b)

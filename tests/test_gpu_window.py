@@ -23,6 +23,14 @@ import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
+# the windowed schedule's max* forms: "logmap" = the one-read table (td_set_window_maxstar default,
+# the C restatement's TDO_ALGO_LOGMAP_Q), "logmap-exact" = log_map.cpp's E_algorithm, "maxlog"
+ALGOS = ["logmap", "logmap-exact", "maxlog"]
+
+
+def _oalgo(algo):
+    return {"logmap": O.ALGO_LOGMAP_Q, "logmap-exact": O.ALGO_LOGMAP, "maxlog": O.ALGO_MAXLOG}[algo]
+
 
 def _decode(K, f1, f2, iters, flow, algo, window, overlap, precision="f64", ext_scale=1.0, nii=False,
             concurrent=False, run=0):
@@ -32,8 +40,9 @@ def _decode(K, f1, f2, iters, flow, algo, window, overlap, precision="f64", ext_
     dt = torch.float64 if precision == "f64" else torch.float32
     x = torch.from_numpy(flow).to("cuda:0").to(dt).contiguous()
     B = flow.shape[0]
-    with TurboCodec(K, f1, f2, iterations=iters, algo=algo, precision=precision) as c:
+    with TurboCodec(K, f1, f2, iterations=iters, algo=algo.split("-")[0], precision=precision) as c:
         c.debug_window_layout(run)
+        c.set_window_maxstar(algo == "logmap-exact")
         c.set_window(window, overlap, ext_scale, nii=nii, concurrent=concurrent)
         bits = torch.empty((B, iters, K), dtype=torch.uint8, device=x.device)
         le = torch.empty((B, iters, 2, K + 3), dtype=dt, device=x.device)
@@ -90,7 +99,7 @@ WIN_CASES = [
 ]
 
 
-@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("K,f1,f2,W,g,nii,conc,scale,run", WIN_CASES)
 def test_window_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale, run, algo):
     """Every schedule option, both algorithms, both lane layouts: bits identical to the C
@@ -98,7 +107,7 @@ def test_window_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale, run, algo):
     B, iters = (3, 3) if K > 2048 else (9, 5)
     _, flow = O.synth_batch(K, f1, f2, 0.3, 11 + W + g, B)
     bits, le = _decode(K, f1, f2, iters, flow, algo, W, g, ext_scale=scale, nii=nii, concurrent=conc, run=run)
-    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    oalgo = _oalgo(algo)
     for b in range(B):
         ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo, nii=nii, concurrent=conc,
                                        scale=scale)
@@ -107,7 +116,7 @@ def test_window_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale, run, algo):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("K,f1,f2,W,g,nii,conc,scale", [
     (1024, 31, 64, 64, 30, False, False, 1.0),
     (512, 31, 64, 48, 48, True, True, 0.77),
@@ -125,7 +134,7 @@ def test_window_single_frame_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale,
     _, flow = O.synth_batch(K, f1, f2, 0.3, 5 + W + g, 2)
     if precision == "f32":
         flow = flow.astype(np.float32)
-    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    oalgo = _oalgo(algo)
     for b in range(2):
         bits, le = _decode(K, f1, f2, iters, flow[b:b + 1], algo, W, g, precision=precision, ext_scale=scale,
                            nii=nii, concurrent=conc)
@@ -136,7 +145,7 @@ def test_window_single_frame_vs_c_restatement(K, f1, f2, W, g, nii, conc, scale,
         assert np.abs(le[0] - ol).max() <= tol, f"frame {b}"
 
 
-@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("run", [0, 3])
 def test_window_f32_vs_c_restatement(algo, run):
     """fp32 (checkpoints and normalisation every 8 positions) against the fp32 restatement."""
@@ -144,7 +153,7 @@ def test_window_f32_vs_c_restatement(algo, run):
     _, flow = O.synth_batch(K, f1, f2, 0.5, 77, B)
     flow = flow.astype(np.float32)
     bits, le = _decode(K, f1, f2, iters, flow, algo, W, g, precision="f32", run=run)
-    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    oalgo = _oalgo(algo)
     for b in range(B):
         ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo)
         assert np.array_equal(bits[b], ob), f"codeword {b}"
@@ -153,6 +162,7 @@ def test_window_f32_vs_c_restatement(algo, run):
 
 @pytest.mark.parametrize("nii,conc,scale,precision,algo", [(False, False, 1.0, "f64", "logmap"),
                                                          (True, True, 0.77, "f64", "logmap"),
+                                                         (False, False, 1.0, "f64", "logmap-exact"),
                                                          (False, False, 1.0, "f32", "logmap"),
                                                          (True, True, 0.77, "f32", "maxlog")])
 def test_window_batch_parts_and_runs_do_not_change_results(nii, conc, scale, precision, algo):
@@ -174,7 +184,8 @@ def test_window_batch_parts_and_runs_do_not_change_results(nii, conc, scale, pre
     x = torch.from_numpy(np.ascontiguousarray(flow)).to("cuda:0")
     outs = {}
     for parts, run_a in ((1, 0), (2, 0), (3, 0), (4, 0), (2, 1), (4, 3)):
-        with TurboCodec(K, f1, f2, iterations=iters, algo=algo, precision=precision) as c:
+        with TurboCodec(K, f1, f2, iterations=iters, algo=algo.split("-")[0], precision=precision) as c:
+            c.set_window_maxstar(algo == "logmap-exact")
             c.set_window(W, g, scale, nii=nii, concurrent=conc)
             c.debug_window_layout(0, run_a, parts)   # after set_window: applies to the current schedule too
             bits = torch.empty((B, K), dtype=torch.uint8, device=x.device)
@@ -186,7 +197,7 @@ def test_window_batch_parts_and_runs_do_not_change_results(nii, conc, scale, pre
     for key, (bk, lk) in outs.items():
         assert np.array_equal(bk, b1), key
         assert np.array_equal(lk, l1), key
-    oalgo = O.ALGO_MAXLOG if algo == "maxlog" else O.ALGO_LOGMAP
+    oalgo = _oalgo(algo)
     for b in (0, 64 * 64 + 5, 2 * 64 * 64 + 11, B - 1):   # one codeword in each of the four parts
         ob, ol = O.turbo_decode_window(flow[b], K, f1, f2, iters, W, g, algo=oalgo, nii=nii, concurrent=conc,
                                        scale=scale)
@@ -196,7 +207,7 @@ def test_window_batch_parts_and_runs_do_not_change_results(nii, conc, scale, pre
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("algo", ["logmap", "maxlog"])
+@pytest.mark.parametrize("algo", ALGOS)
 def test_window_high_snr_ragged_batch_error_free(algo, precision):
     """Ragged batch (B = 13) at 3 dB: every codeword decodes without error by the last iteration."""
     K, f1, f2, B = 6144, 263, 480, 13
@@ -207,7 +218,8 @@ def test_window_high_snr_ragged_batch_error_free(algo, precision):
     assert np.array_equal(bits[:, -1, :], info.astype(np.uint8))
 
 
-def test_window_ber_close_to_exact():
+@pytest.mark.parametrize("table", ["fast", "exact"])
+def test_window_ber_close_to_exact(table):
     """north_star's gate for config 5 ("BER-vs-Eb/N0 within 0.05 dB of the CPU reference"), on the
     waterfall: K=6144, 8 iterations, the same 32768 generator frames at 0.35 and 0.40 dB through the
     exact schedule (bit-exact against the reference) and the windowed one (W = 64, overlap 30).
@@ -223,6 +235,7 @@ def test_window_ber_close_to_exact():
     K, f1, f2, B, iters = 6144, 263, 480, 32768, 8
     res = {}
     with TurboCodec(K, f1, f2, iterations=iters) as ex, TurboCodec(K, f1, f2, iterations=iters) as win:
+        win.set_window_maxstar(table == "exact")
         win.set_window(64, 30, 1.0)
         for k, e in enumerate((0.35, 0.40)):
             ex.synth_seed(100 + k)
@@ -350,6 +363,6 @@ def test_config5_full_batch():
         bs, ls, fs = bits[idx].cpu().numpy(), le[idx].cpu().numpy(), llr[idx].cpu().numpy()
     del bits, le, llr
     for k in range(len(sample)):
-        ob, ol = O.turbo_decode_window(fs[k], K, f1, f2, iters, 64, 30)
+        ob, ol = O.turbo_decode_window(fs[k], K, f1, f2, iters, 64, 30, algo=O.ALGO_LOGMAP_Q)
         assert np.array_equal(bs[k], ob), f"codeword {sample[k]} (log-MAP)"
         assert np.abs(ls[k] - ol).max() <= 1e-9, f"codeword {sample[k]} (log-MAP)"

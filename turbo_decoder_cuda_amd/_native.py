@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("TD_LIB_PATH") or os.path.join(PKG, "libturbo_mi355x.s
 TD_OK, TD_EINVAL, TD_ENOMEM, TD_EHIP, TD_ENODEV = 0, 1, 2, 3, 4
 TD_ALGO_LOGMAP, TD_ALGO_MAXLOG = 0, 1
 TD_F64, TD_F32 = 0, 1
+TD_WMAXSTAR_FAST, TD_WMAXSTAR_EXACT = 0, 1
+TD_MAXSTAR_WINDOW_FAST = 2   # td_maxstar_host_* algo: the windowed one-read table
 
 # every symbol include/turbo_mi355x.h declares (tests check the .so exports all of them)
 EXPORTS = (
@@ -23,7 +25,7 @@ EXPORTS = (
     "td_debug_stamp_slots", "td_synth_seed", "td_synth_frames", "td_count_errors", "td_rand_window", "td_synth_seek",
     "td_set_window", "td_synth_modulation", "td_modulate", "td_demodulate", "td_debug_placement",
     "td_debug_placement_rule", "td_clock_read", "td_window_steps", "td_debug_placement_cost", "td_debug_window_layout",
-    "td_debug_workspace_bytes",
+    "td_debug_workspace_bytes", "td_set_window_maxstar",
 )
 
 

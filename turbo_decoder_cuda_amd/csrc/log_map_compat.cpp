@@ -23,6 +23,8 @@
 //   TD_OVERLAP=g    warm-up steps of each sub-block's alpha / beta (default min(30, 3W))
 //   TD_NII=1        boundary metrics from the previous iteration
 //   TD_CONCURRENT=1 both SISOs at once (Jacobi); TD_EXT_SCALE=s extrinsic scale (default 1)
+//   TD_WINDOW_MAXSTAR=exact  log_map.cpp's E_algorithm in the windowed log-MAP schedule (default: the
+//                   one-read table, td_set_window_maxstar)
 // A windowed schedule changes the arithmetic (sub-block boundaries): its results are gated by
 // the BER curve, not bit-exact.  Log_MAP_decoder always runs the exact SISO.
 #include <cstdio>
@@ -71,7 +73,10 @@ void set_schedule(td_handle* h)
     w.nii = env_int("TD_NII", 0);
     w.concurrent = env_int("TD_CONCURRENT", 0);
     w.ext_scale = env_double("TD_EXT_SCALE", 1.0);
-    const int rc = td_set_window(h, &w);
+    const char* ms = std::getenv("TD_WINDOW_MAXSTAR");
+    int rc = td_set_window_maxstar(h, ms && std::strcmp(ms, "exact") == 0 ? TD_WMAXSTAR_EXACT : TD_WMAXSTAR_FAST);
+    if (rc) die("td_set_window_maxstar (TD_WINDOW_MAXSTAR)", rc);
+    rc = td_set_window(h, &w);
     if (rc) die("td_set_window (TD_WINDOW / TD_OVERLAP / TD_EXT_SCALE)", rc);
 }
 

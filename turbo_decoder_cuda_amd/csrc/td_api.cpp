@@ -59,6 +59,7 @@ struct td_handle {
     int* d_pi = nullptr;
     int* d_pinv = nullptr;
     void* d_lut = nullptr;
+    void* d_qlut = nullptr;        // the windowed schedule's one-read max* table (build_qlut), handle precision
     td::LaneTables* d_lane = nullptr;
     unsigned* d_slots = nullptr;   // per-CU occupancy bits of the turbo kernel (wg_pos)
     unsigned long long* d_clk = nullptr;   // the last decode's clock sample (td_clock_read)
@@ -94,6 +95,7 @@ struct td_handle {
     // decoding schedule (td_set_window): window 0 = exact full trellis
     td::WindowParams wp{0, 0, 0, 0, 1.0, 0};
     int win_run = 0, win_run_a = 0, win_parts = 0;   // td_debug_window_layout (tests, measurements)
+    int win_exact_table = 0;                         // td_set_window_maxstar
     void* d_wws = nullptr;   // windowed-schedule buffers (second extrinsic pair, NII metrics)
     size_t wws_bytes = 0;
     td::WindowStreams wstr{};                    // the windowed schedule's extra streams (batch parts)
@@ -163,6 +165,7 @@ void fill_common(td::DecodeParams<T>& dp, const td_handle* h)
     std::memcpy(dp.nextout, h->tr.nextout, sizeof dp.nextout);
     dp.lane = h->d_lane;
     dp.lut = static_cast<const td::LutEntry<T>*>(h->d_lut);
+    dp.qlut = static_cast<const T*>(h->d_qlut);
     dp.algo = h->p.algo;
     dp.role_cus = h->role_cus;
     dp.occ3 = h->occ3;
@@ -740,18 +743,22 @@ int td_qpp_table(int K, int f1, int f2, int* pi)
 double td_maxstar_host_f64(double x, double y, int algo)
 {
     static td::LutEntry<double> lut[td::kLutSize];
-    static bool init = (td::build_lut<double>(lut), true);
+    static double q[td::kQRows];
+    static bool init = (td::build_lut<double>(lut), td::build_qlut<double>(q), true);
     (void)init;
     if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
+    if (algo == TD_MAXSTAR_WINDOW_FAST) return td::maxstar_qlut_host<double>(x, y, q);
     return td::maxstar_lut_host<double>(x, y, lut);
 }
 
 float td_maxstar_host_f32(float x, float y, int algo)
 {
     static td::LutEntry<float> lut[td::kLutSize];
-    static bool init = (td::build_lut<float>(lut), true);
+    static float q[td::kQRows];
+    static bool init = (td::build_lut<float>(lut), td::build_qlut<float>(q), true);
     (void)init;
     if (algo == TD_ALGO_MAXLOG) return x > y ? x : y;
+    if (algo == TD_MAXSTAR_WINDOW_FAST) return td::maxstar_qlut_host<float>(x, y, q);
     return td::maxstar_lut_host<float>(x, y, lut);
 }
 
@@ -811,6 +818,7 @@ int td_create(td_handle** out, const td_params* p)
     if (hipMalloc(&h->d_pi, sizeof(int) * (p->K + td::kPermPad)) != hipSuccess ||
         hipMalloc(&h->d_pinv, sizeof(int) * (p->K + td::kPermPad)) != hipSuccess ||
         hipMalloc(&h->d_lut, sizeof(td::LutEntry<double>) * td::kLutSize) != hipSuccess ||
+        hipMalloc(&h->d_qlut, sizeof(double) * td::kQRows) != hipSuccess ||
         hipMalloc(&h->d_lane, sizeof(td::LaneTables)) != hipSuccess ||
         hipMalloc(&h->d_slots, sizeof(unsigned) * td::kCuSlotKeys) != hipSuccess ||
         hipMalloc(&h->d_clk, 4 * sizeof(unsigned long long)) != hipSuccess) {
@@ -832,11 +840,17 @@ int td_create(td_handle** out, const td_params* p)
         if (p->precision == TD_F64) {
             td::LutEntry<double> lut[td::kLutSize];
             td::build_lut<double>(lut);
+            double q[td::kQRows];
+            td::build_qlut<double>(q);
             e = hipMemcpy(h->d_lut, lut, sizeof lut, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(h->d_qlut, q, sizeof q, hipMemcpyHostToDevice);
         } else {
             td::LutEntry<float> lut[td::kLutSize];
             td::build_lut<float>(lut);
+            float q[td::kQRows];
+            td::build_qlut<float>(q);
             e = hipMemcpy(h->d_lut, lut, sizeof lut, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(h->d_qlut, q, sizeof q, hipMemcpyHostToDevice);
         }
     }
     if (e != hipSuccess) {
@@ -855,6 +869,7 @@ int td_destroy(td_handle* h)
     if (h->d_pi) (void)hipFree(h->d_pi);
     if (h->d_pinv) (void)hipFree(h->d_pinv);
     if (h->d_lut) (void)hipFree(h->d_lut);
+    if (h->d_qlut) (void)hipFree(h->d_qlut);
     if (h->d_lane) (void)hipFree(h->d_lane);
     if (h->d_slots) (void)hipFree(h->d_slots);
     if (h->d_clk) (void)hipFree(h->d_clk);
@@ -894,7 +909,7 @@ int td_set_window(td_handle* h, const td_window_params* w)
 {
     if (!h) return fail(TD_EINVAL, "td_set_window: null handle");
     if (!w || w->window == 0) {
-        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0, 0, 0};
+        h->wp = td::WindowParams{0, 0, 0, 0, 1.0, 0, 0, 0, 0};
         return TD_OK;
     }
     if (w->window < 3 || w->window > 10000) return fail(TD_EINVAL, "td_set_window: window must be 0 or in [3, 10000]");
@@ -906,7 +921,17 @@ int td_set_window(td_handle* h, const td_window_params* w)
     const int rc = ensure_wstr(h);
     if (rc) return rc;
     h->wp = td::WindowParams{w->window, w->overlap, w->nii ? 1 : 0, w->concurrent ? 1 : 0, w->ext_scale,
-                             h->win_run, h->win_run_a, h->win_parts};
+                             h->win_run, h->win_run_a, h->win_parts, h->win_exact_table};
+    return TD_OK;
+}
+
+int td_set_window_maxstar(td_handle* h, int form)
+{
+    if (!h) return fail(TD_EINVAL, "td_set_window_maxstar: null handle");
+    if (form != TD_WMAXSTAR_FAST && form != TD_WMAXSTAR_EXACT)
+        return fail(TD_EINVAL, "td_set_window_maxstar: form must be TD_WMAXSTAR_FAST or TD_WMAXSTAR_EXACT");
+    h->win_exact_table = form == TD_WMAXSTAR_EXACT ? 1 : 0;
+    h->wp.exact_table = h->win_exact_table;
     return TD_OK;
 }
 

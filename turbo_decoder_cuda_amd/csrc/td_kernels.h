@@ -63,6 +63,7 @@ struct DecodeParams {
     const int* pi;              // [K] QPP
     const int* pinv;            // [K] inverse QPP
     const LutEntry<T>* lut;     // [kLutSize]
+    const T* qlut;              // [kQRows] the windowed schedule's one-read max* table (build_qlut)
     uint8_t* bits;              // decisions (see td_decode_device)
     T* le_dump;                 // nullable
     unsigned long long* stamps; // diagnostic build (TD_STAMPS) only: [G][6] phase cycle totals
@@ -101,9 +102,11 @@ struct WindowParams {
     int nii;           // boundary metrics from the previous iteration
     int concurrent;    // both SISOs per launch on the previous iteration's extrinsics
     double ext_scale;  // extrinsic scaling (1 = none)
-    int run;           // sub-blocks per lane run, 0 = chosen by window_run (TD_WINDOW_RUN, tests)
-    int run_a;         // the alpha kernel's, if non-zero (TD_WINDOW_RUN_A, measurements)
-    int parts;         // batch parts on as many streams, 0 = 2 (TD_WINDOW_PARTS, measurements)
+    int run;           // sub-blocks per lane run, 0 = chosen by window_run (td_debug_window_layout)
+    int run_a;         // the alpha kernel's, if non-zero (td_debug_window_layout)
+    int parts;         // batch parts on as many streams, 0 = 2 (td_debug_window_layout)
+    int exact_table;   // 1: log-MAP with log_map.cpp's E_algorithm exactly (three-read bucket table);
+                       // 0: the one-read table of build_qlut (td_set_window_maxstar)
 };
 // extra device buffers of the windowed schedule
 template <typename T>

@@ -2326,31 +2326,73 @@ struct SwLut {
 static_assert(SwLut<double>::kOffV % 512 && (SwLut<double>::kOffH - SwLut<double>::kOffV) % 512 &&
                   SwLut<double>::kOffH % 512 && SwLut<double>::kOffV > 2040, "no ds_read2 merging");
 
+// The one-read table (ALGO 2, round 6; td_tables.h build_qlut): one value per bucket of the finer grid
+// (exponent + kQBits mantissa bits), the same 32 replicated columns, so one conflict-free ds_read_b64
+// per max* and no threshold compare / select.
 template <typename T>
+struct SwQLut {
+    static constexpr int kCols = 32;
+    static constexpr int kRow = kCols * (int)sizeof(T);
+    static constexpr int kBytes = kQRows * kRow;
+};
+// LDS bytes of the windowed kernels' max* table for ALGO (0: three-read exact, 1: none, 2: one-read)
+template <typename T, int ALGO>
+constexpr int sw_lut_bytes()
+{
+    return ALGO == 0 ? SwLut<T>::kBytes : (ALGO == 2 ? SwQLut<T>::kBytes : 16);
+}
+
+template <typename T, int ALGO>
 __device__ __forceinline__ void sw_lut_fill(char* lut_s, const DecodeParams<T>& p)
 {
-    using Lt = SwLut<T>;
-    for (int e = threadIdx.x; e < Lt::kRows * Lt::kCols; e += blockDim.x) {
-        const int q = e / Lt::kCols, o = q * Lt::kRow + (e % Lt::kCols) * (int)sizeof(T);
-        const LutEntry<T>& last = p.lut[kLutSize - 1];
-        *reinterpret_cast<T*>(lut_s + o) = q < kLutSize ? (T)p.lut[q].thr : (T)INFINITY;
-        *reinterpret_cast<T*>(lut_s + Lt::kOffV + o) = q < kLutSize ? (T)p.lut[q].vlo : (T)last.vhi;
-        *reinterpret_cast<T*>(lut_s + Lt::kOffH + o) = q < kLutSize ? (T)p.lut[q].vhi : (T)last.vhi;
+    if constexpr (ALGO == 2) {
+        using Lq = SwQLut<T>;
+        for (int e = threadIdx.x; e < kQRows * Lq::kCols; e += blockDim.x)
+            *reinterpret_cast<T*>(lut_s + (e / Lq::kCols) * Lq::kRow + (e % Lq::kCols) * (int)sizeof(T)) =
+                p.qlut[e / Lq::kCols];
+    } else if constexpr (ALGO == 0) {
+        using Lt = SwLut<T>;
+        for (int e = threadIdx.x; e < Lt::kRows * Lt::kCols; e += blockDim.x) {
+            const int q = e / Lt::kCols, o = q * Lt::kRow + (e % Lt::kCols) * (int)sizeof(T);
+            const LutEntry<T>& last = p.lut[kLutSize - 1];
+            *reinterpret_cast<T*>(lut_s + o) = q < kLutSize ? (T)p.lut[q].thr : (T)INFINITY;
+            *reinterpret_cast<T*>(lut_s + Lt::kOffV + o) = q < kLutSize ? (T)p.lut[q].vlo : (T)last.vhi;
+            *reinterpret_cast<T*>(lut_s + Lt::kOffH + o) = q < kLutSize ? (T)p.lut[q].vhi : (T)last.vhi;
+        }
     }
     __syncthreads();
 }
 // this lane's table origin: its column, shifted down by the first bucket's field value
-template <typename T>
+template <typename T, int ALGO>
 __device__ __forceinline__ const char* sw_lut_lane(const char* lut_s, int lane)
 {
+    if constexpr (ALGO == 2)
+        return lut_s + (lane % SwQLut<T>::kCols) * (int)sizeof(T) - QBucketBits<T>::base * SwQLut<T>::kRow;
     return lut_s + (lane % SwLut<T>::kCols) * (int)sizeof(T) - BucketBits<T>::base * SwLut<T>::kRow;
 }
-// E_algorithm (log_map.cpp:779-801) in the exact bucket form of mstar, on the windowed table
+// the one-read table's clamped row field of d (sign outside the field, as bucket_dev)
+template <typename T>
+__device__ __forceinline__ int qbucket_dev(T d)
+{
+    using QB = QBucketBits<T>;
+    unsigned hi;
+    if constexpr (sizeof(T) == 8)
+        hi = (unsigned)((unsigned long long)__double_as_longlong(d) >> 32);
+    else
+        hi = (unsigned)__float_as_int(d);
+    const int q = (int)__builtin_amdgcn_ubfe(hi, QB::shift, QB::width);
+    return min(max(q, QB::base), QB::base + kQRows - 1);
+}
+// max* of the windowed schedule: ALGO 0 E_algorithm (log_map.cpp:779-801) in the exact bucket form of
+// mstar; ALGO 1 max (Max-Log-MAP); ALGO 2 the one-read table (td_tables.h build_qlut)
 template <typename T, int ALGO>
 __device__ __forceinline__ T sw_mstar(T x, T y, const char* lut)
 {
     if constexpr (ALGO == 1) {
         return vmax(x, y);
+    } else if constexpr (ALGO == 2) {
+        const T d = y - x;
+        return vmax(x, y) + *reinterpret_cast<const T*>(lut + qbucket_dev<T>(d) * SwQLut<T>::kRow);
     } else {
         using Lt = SwLut<T>;
         const T d = y - x;
@@ -2574,12 +2616,12 @@ __device__ __forceinline__ T* sw_ck(const WinArgs<T>& a, const SwTask& t, int s,
 template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
-    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
-    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    __shared__ alignas(16) char lut_s[sw_lut_bytes<T, ALGO>()];
+    if constexpr (ALGO != 1) sw_lut_fill<T, ALGO>(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
-    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    const char* lut = sw_lut_lane<T, ALGO>(lut_s, lane);
     const int W = a.W, g = a.g, nS = a.nS, L = p.L, dec = t.dec, cwv = t.cwv;
     T* const niw = a.nii_wr + ((size_t)dec * a.Bp + t.b) * nS * 16;
     const T* const nir = a.nii_rd + ((size_t)dec * a.Bp + t.b) * nS * 16;
@@ -2781,13 +2823,13 @@ __device__ __forceinline__ T sw_lps_norm(T v, int lane)
 template <typename T, int ALGO, int S>
 __global__ __launch_bounds__(256) void sw_alpha_lps_kernel(DecodeParams<T> p, WinArgs<T> a)
 {
-    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
+    __shared__ alignas(16) char lut_s[sw_lut_bytes<T, ALGO>()];
     __shared__ T lin_s[4][3][kSwLpsChunk];   // per wave: codeword 0's ys, yp, La of a chunk of positions
-    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    if constexpr (ALGO != 1) sw_lut_fill<T, ALGO>(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
-    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    const char* lut = sw_lut_lane<T, ALGO>(lut_s, lane);
     T (&lin)[3][kSwLpsChunk] = lin_s[threadIdx.x >> 6];
     SwLps l;
     l.j = lane & 7;
@@ -2957,15 +2999,15 @@ template <typename T, int ALGO, int S, bool LF>
 __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodeParams<T> p, WinArgs<T> a, const int* __restrict__ pi,
                                                       const int* __restrict__ pinv)
 {
-    __shared__ alignas(16) char lut_s[ALGO == 0 ? SwLut<T>::kBytes : 16];
+    __shared__ alignas(16) char lut_s[sw_lut_bytes<T, ALGO>()];
     __shared__ alignas(16) T ck_lds[4 * 8 * 64];   // per wave: the next segment's checkpoint (DMA slot)
     __shared__ alignas(16) T in_lds[4 * 3 * S * 64];   // per wave: the next segment's ys, yp, La rows (DMA slot)
     __shared__ alignas(16) int ix_lds[4 * 64];         // per wave: the next segment's interleaver entries (DMA slot)
-    if constexpr (ALGO == 0) sw_lut_fill(lut_s, p);
+    if constexpr (ALGO != 1) sw_lut_fill<T, ALGO>(lut_s, p);
     SwTask t;
     if (!sw_task(p, a, t)) return;
     const int lane = threadIdx.x & 63;
-    const char* lut = sw_lut_lane<T>(lut_s, lane);
+    const char* lut = sw_lut_lane<T, ALGO>(lut_s, lane);
     const int W = a.W, g = a.g, nS = a.nS, L = p.L, K = p.K, dec = t.dec, cwv = t.cwv;
     const int col = LF ? 0 : lane;                // this lane's codeword within the wave
     const int b = LF ? t.cwv * 64 : t.b;
@@ -3494,7 +3536,8 @@ template <typename T>
 hipError_t launch_window(const DecodeParams<T>& p, const WindowParams& w, const WindowBufs<T>& wb, hipStream_t st,
                          const WindowStreams& ws)
 {
-    return p.algo == 1 ? launch_window_algo<T, 1>(p, w, wb, st, ws) : launch_window_algo<T, 0>(p, w, wb, st, ws);
+    if (p.algo == 1) return launch_window_algo<T, 1>(p, w, wb, st, ws);
+    return w.exact_table ? launch_window_algo<T, 0>(p, w, wb, st, ws) : launch_window_algo<T, 2>(p, w, wb, st, ws);
 }
 
 #endif  // TD_WIN_TU

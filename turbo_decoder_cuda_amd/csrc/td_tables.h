@@ -219,4 +219,70 @@ inline T maxstar_lut_host(T x, T y, const LutEntry<T>* lut)
     return m + (d >= lut[q].thr ? hi : lut[q].vlo);
 }
 
+// ---- The windowed schedule's one-read max* table (round 6; td_set_window_maxstar).
+// The sub-block schedule is BER-gated, not bit-exact (its boundaries already change the arithmetic),
+// so its max* may take the reference's 16-step correction (log_map.cpp:14-18, 779-801) with each
+// threshold moved to the nearest edge of a finer bucket grid: exponent + kQBits mantissa bits of d
+// (8 buckets an octave), one correction value per bucket -- the reference's value at the bucket's
+// midpoint.  Then f(d) is ONE table read at the bucket's row: no threshold read, compare and select
+// (3 of a table max*'s 11 VALU and 2 of its 3 LDS reads).  The correction differs from E_algorithm's
+// only for d within half a bucket (6.25 % of d) of one of its 15 thresholds, by one table step.
+//   row 0             d < 2^-4 (1 + 2^-kQBits) (and every smaller d)
+//   rows 1 .. 7*2^k-1 [2^e (1 + m/2^k), 2^e (1 + (m+1)/2^k)),  e = -4..2
+//   row 7*2^k         d >= 8  (f = 0)
+constexpr int kQBits = 3;
+constexpr int kQRows = (7 << kQBits) + 1;
+
+template <typename T>
+struct QBucketBits;
+template <>
+struct QBucketBits<double> {   // bits 17..30 of the high dword: 11 exponent + 3 mantissa bits
+    static constexpr int shift = 20 - kQBits, width = 11 + kQBits, base = (1023 - 4) << kQBits;
+};
+template <>
+struct QBucketBits<float> {    // bits 20..30: 8 exponent + 3 mantissa bits
+    static constexpr int shift = 23 - kQBits, width = 8 + kQBits, base = (127 - 4) << kQBits;
+};
+
+inline int qbucket_of_bits(unsigned hi, int shift, int width, int base)
+{
+    int q = (int)((hi >> shift) & ((1u << width) - 1)) - base;
+    return q < 0 ? 0 : (q > kQRows - 1 ? kQRows - 1 : q);
+}
+
+// E_algorithm's correction f(d) for d >= 0 (log_map.cpp:784-797: the linear scan; 0 past the last index)
+inline double reference_correction(double d)
+{
+    if (d >= kIdx[15]) return 0.0;
+    int i = 1;
+    while (i < 16 && !(d < kIdx[i])) ++i;
+    return kTab[i - 1];
+}
+
+// the table: row q's value = the reference's correction at the row's midpoint (rounded once to T)
+template <typename T>
+inline void build_qlut(T* v)
+{
+    for (int q = 0; q < kQRows; ++q) {
+        if (q == kQRows - 1) {
+            v[q] = (T)0;
+            continue;
+        }
+        const int e = q >> kQBits, m = q & ((1 << kQBits) - 1);
+        const double lo = std::ldexp(1.0 + (double)m / (1 << kQBits), e - 4);
+        const double hi = std::ldexp(1.0 + (double)(m + 1) / (1 << kQBits), e - 4);
+        v[q] = (T)reference_correction(0.5 * (lo + hi));
+    }
+}
+
+// Host evaluation of the one-read max* as the windowed kernels evaluate it (td_kernels.hip sw_mstar)
+template <typename T>
+inline T maxstar_qlut_host(T x, T y, const T* v)
+{
+    using QB = QBucketBits<T>;
+    const T d = y - x;
+    const T m = x > y ? x : y;
+    return m + v[qbucket_of_bits(high_word(d), QB::shift, QB::width, QB::base)];
+}
+
 }  // namespace td

@@ -91,6 +91,11 @@ class TurboCodec:
         N.check(N.lib().td_debug_workspace_bytes(self._h, C.byref(v)))
         return int(v.value)
 
+    def set_window_maxstar(self, exact: bool) -> None:
+        """max* of the windowed log-MAP schedule (td_set_window_maxstar): exact=False the one-read
+        table (default), exact=True log_map.cpp's E_algorithm exactly."""
+        N.check(N.lib().td_set_window_maxstar(self._h, N.TD_WMAXSTAR_EXACT if exact else N.TD_WMAXSTAR_FAST))
+
     def set_window(self, window: int = 64, overlap: int = 30, ext_scale: float = 1.0, nii: bool = False,
                    concurrent: bool = False) -> None:
         """Windowed schedule (td_set_window; BASELINE config 5); window=0: exact.
