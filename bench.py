@@ -144,7 +144,7 @@ def window_roofline(K, B, iters, decode_ms, sclk_ghz=None, sclk_source=None, exa
     """Roofline record of the windowed schedule (BASELINE config 5: fp64 log-MAP, window 64, overlap 30)
     from the live decode time and the committed PMC of the same kernels (profiles/traffic.json key
     K6144_B32768_it8_f64_logmap_w64g30: FETCH_SIZE x2 + WRITE_SIZE bytes and SQ_INSTS_VALU per decode,
-    scripts/gpu_r5_wpmc.sh).  Two bounds: VALU issue (a wave64 fp64 VALU instruction occupies its SIMD
+    scripts/gpu_window_pmc.sh).  Two bounds: VALU issue (a wave64 fp64 VALU instruction occupies its SIMD
     4 cycles; 1024 SIMDs at the shader clock) and HBM (counter bytes against the 8 TB/s spec and the
     6.29 TB/s streaming ceiling).  The algorithmic-bytes fraction is the metric's contract, as for
     the exact kernel."""

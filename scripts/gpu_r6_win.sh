@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the windowed schedule's one-read max* table.  Parity of every window test (both max*
 # forms against the C restatement), the paired BER curve of both forms against the exact schedule,
-# the bench's config-5 lines, then the PMC of the new default (scripts/gpu_r5_wpmc.sh).
+# the bench's config-5 lines, then the PMC of the new default (scripts/gpu_window_pmc.sh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_handle.py tests/test_gpu_decode.py -k "window or graph" \
@@ -22,5 +22,5 @@ for k, v in d["variants"].items():
 dr = d.get("dropin", {})
 print("dropin", dr.get("ms_per_frame"), (dr.get("window") or {}).get("ms_per_frame"), (dr.get("window") or {}).get("bit_errors"))
 PY
-bash scripts/gpu_r5_wpmc.sh > gpurun_out/r6_wpmc.txt 2>&1
+bash scripts/gpu_window_pmc.sh > gpurun_out/r6_wpmc.txt 2>&1
 rc=$?; cat gpurun_out/r6_wpmc.txt; exit $rc

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: PMC of the windowed kernels (config 5) for one library (LIB), one pass per counter group
+# PMC of the windowed kernels (BASELINE config 5) for one library (LIB), one pass per counter group
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 mkdir -p gpurun_out/wpmc

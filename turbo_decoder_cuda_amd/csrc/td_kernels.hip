@@ -71,6 +71,8 @@ constexpr unsigned kDiagNoBConvert = 2;   // the B pass without the loader's til
 constexpr unsigned kDiagNoFold = 4;       // the B pass without its folds
 constexpr unsigned kDiagNoBeta = 8;       // the B pass without the beta chain
 constexpr unsigned kDiagOcc3Alias = 16;   // beta rows and tile ring alias the alpha ring: fp64 three per CU (Smem)
+constexpr unsigned kDiagNoAStore = 32;    // the F pass without its alpha scratch stores (power / clock attribution)
+constexpr unsigned kDiagFoldNoLut = 64;   // the B pass's folds with a table-free max* (no LDS reads; LDS contention test)
 template <unsigned D>
 constexpr bool kDiag = (TD_DIAG & D) != 0;
 
@@ -1039,7 +1041,7 @@ struct AlphaSched {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (K + 2 < kW) op[(K + 2) % 3] = alpha_in<T, (K + 2) % 3>(sm, tb, K + 2, c, lc);
         __builtin_amdgcn_sched_barrier(0);
-        gstore(ga + K * kLanes + lc.st_off[PH], a);   // alpha_raw[.][i]
+        if constexpr (!kDiag<kDiagNoAStore>) gstore(ga + K * kLanes + lc.st_off[PH], a);   // alpha_raw[.][i]
         __builtin_amdgcn_sched_barrier(0);
         a = sched_finish(xs, xp, d, thr, lo, hi);
         AlphaSched<T, K + 1>::run(a, op, sm, tb, lut, c, lc, ga);
@@ -1089,7 +1091,7 @@ __device__ __forceinline__ void tm_keep(TmBatch<T>& tbh, T m, T* stm)
 template <typename T, int K>
 __device__ __forceinline__ void astore_row(T* sa, unsigned voff, T v)
 {
-    gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
+    if constexpr (!kDiag<kDiagNoAStore>) gstore_s<(K - kArow0) * kLanes * (int)sizeof(T)>(sa, voff, v);
 }
 
 // Log-MAP, speculative table row (kASpec): the step's max* row is read from the bucket of the
@@ -1532,6 +1534,16 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     if constexpr (ALGO == 1) {   // Max-Log-MAP: a max tree (exact in any order), as fold_item
         r0 = vmax(vmax(vmax(t0[0], t0[1]), vmax(t0[2], t0[3])), vmax(vmax(t0[4], t0[5]), vmax(t0[6], t0[7])));
         r1 = vmax(vmax(vmax(t1[0], t1[1]), vmax(t1[2], t1[3])), vmax(vmax(t1[4], t1[5]), vmax(t1[6], t1[7])));
+    } else if constexpr (kDiag<kDiagFoldNoLut>) {
+        // diagnostic (results wrong): the same dependent chain without its table reads
+        auto ms = [](T x, T y) { const T d = y - x; return vmax(x, y) + (fabs(d) >= (T)0.5 ? (T)0.25 : (T)0.5); };
+        r0 = ms(t0[0], t0[1]);
+        r1 = ms(t1[0], t1[1]);
+#pragma unroll
+        for (int j = 2; j < 8; ++j) {
+            r0 = ms(r0, t0[j]);
+            r1 = ms(r1, t1[j]);
+        }
     } else {
         r0 = mstar<T, ALGO>(t0[0], t0[1], lut);
         r1 = mstar<T, ALGO>(t1[0], t1[1], lut);
