@@ -73,6 +73,7 @@ constexpr unsigned kDiagNoBeta = 8;       // the B pass without the beta chain
 constexpr unsigned kDiagOcc3Alias = 16;   // beta rows and tile ring alias the alpha ring: fp64 three per CU (Smem)
 constexpr unsigned kDiagNoAStore = 32;    // the F pass without its alpha scratch stores (power / clock attribution)
 constexpr unsigned kDiagFoldNoLut = 64;   // the B pass's folds with a table-free max* (no LDS reads; LDS contention test)
+constexpr unsigned kDiagSwNoCk = 128;     // windowed kernels: no alpha checkpoint stores / loads (HBM share test)
 template <unsigned D>
 constexpr bool kDiag = (TD_DIAG & D) != 0;
 
@@ -2696,7 +2697,8 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
             if (bp >= st) {                               // checkpoint alpha[bp] (normalised)
                 T* ck = sw_ck(a, t, s, (bp - st) / S);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) ck[j * 64] = al[j];
+                for (int j = 0; j < 8; ++j)
+                    if constexpr (!kDiag<kDiagSwNoCk>) ck[j * 64] = al[j];
             }
             if (aAll && bAll) {
 #pragma unroll
@@ -2740,7 +2742,8 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
                 if (m == 0 && pos >= st && pos < en) {       // checkpoint alpha[pos] (normalised)
                     T* ck = sw_ck(a, t, s, (pos - st) / S);
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) ck[j * 64] = al[j];
+                    for (int j = 0; j < 8; ++j)
+                        if constexpr (!kDiag<kDiagSwNoCk>) ck[j * 64] = al[j];
                 }
                 if (s < nS - 1 && pos == qb && t.live)
 #pragma unroll
@@ -3114,7 +3117,8 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             const char* src = reinterpret_cast<const char*>(sw_ck(a, t, ns, (nbp - nst) / S) - lane) + lane * 16;
             constexpr int kDma = 8 * 64 * (int)sizeof(T) / 1024;
 #pragma unroll
-            for (int q = 0; q < kDma; ++q) dma16(ckslot_lds + q * 1024, src + q * 1024);
+            for (int q = 0; q < kDma; ++q)
+                if constexpr (!kDiag<kDiagSwNoCk>) dma16(ckslot_lds + q * 1024, src + q * 1024);
         }
         const size_t row = (size_t)cwv * L + nbp, rowk = (size_t)cwv * K + nbp;
         const char* src0 = reinterpret_cast<const char*>((dec ? p.sys2 : p.sys1) + row * kSwCw) + lane * 16;
