@@ -42,6 +42,11 @@ int main()
         CHECK(td_maxstar_host_f64(0.25, 0.25 + d, TD_ALGO_MAXLOG) == std::fmax(0.25, 0.25 + d));
         const float rf = td_maxstar_host_f32(0.25f, 0.25f + (float)d, TD_ALGO_LOGMAP);
         CHECK(rf >= std::fmax(0.25f, 0.25f + (float)d));
+        // the windowed schedule's one-read table (the bucket clamp at both ends included)
+        const double q = td_maxstar_host_f64(0.25, 0.25 + d, TD_MAXSTAR_WINDOW_FAST);
+        CHECK(q >= std::fmax(0.25, 0.25 + d) && q <= std::fmax(0.25, 0.25 + d) + 0.69316);
+        CHECK(std::fabs(q - r) <= 0.05 + 1e-12);
+        CHECK(td_maxstar_host_f32(0.25f, 0.25f + (float)d, TD_MAXSTAR_WINDOW_FAST) >= std::fmax(0.25f, 0.25f + (float)d));
     }
     uint32_t win[31];
     for (unsigned seed : {0u, 1u, 20261015u})
@@ -78,6 +83,9 @@ int main()
     CHECK(td_decode_host(nullptr, nullptr, 1, nullptr, nullptr) == TD_EINVAL);
     CHECK(td_siso_host(nullptr, nullptr, nullptr, 1, nullptr, 43, 1) == TD_EINVAL);
     CHECK(td_set_window(nullptr, nullptr) == TD_EINVAL);
+    CHECK(td_set_window_maxstar(nullptr, TD_WMAXSTAR_FAST) == TD_EINVAL);
+    CHECK(td_debug_window_layout(nullptr, 0, 0, 0) == TD_EINVAL);
+    CHECK(td_debug_workspace_bytes(nullptr, nullptr) == TD_EINVAL);
     CHECK(td_profile_enable(nullptr, 1) == TD_EINVAL);
     CHECK(td_synth_seed(nullptr, 1) == TD_EINVAL);
     CHECK(td_modulate(nullptr, 1, 1, nullptr, nullptr, nullptr) == TD_EINVAL);

@@ -162,6 +162,9 @@ def test_null_handle_calls_are_errors():
     assert L.td_decode_device(None, None, 1, None, 0, None, None) == N.TD_EINVAL
     assert L.td_destroy(None) == 0
     assert L.td_clock_read(None, None, None) == N.TD_EINVAL
+    assert L.td_set_window_maxstar(None, 0) == N.TD_EINVAL
+    assert L.td_debug_window_layout(None, 0, 0, 0) == N.TD_EINVAL
+    assert L.td_debug_workspace_bytes(None, None) == N.TD_EINVAL
 
 
 def test_window_steps_is_the_kernel_window():

@@ -38,6 +38,60 @@ def test_reserve_placement_search_decodes_like_the_oracle(monkeypatch):
     assert np.array_equal(bits.cpu().numpy(), ob)
 
 
+def test_placement_search_holds_at_most_three_workspaces(monkeypatch):
+    """Round 6: the search recycles candidates, so however many it probes it
+    holds at most three workspaces plus a 48 MiB spacer per recycled candidate; the kept candidate is
+    the fastest probed; and the chosen workspace decodes like the oracle."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    monkeypatch.setenv("TD_PLACEMENT_TRIALS", "7")
+    monkeypatch.setenv("TD_PLACEMENT_MIN", "100")   # no early stop: all 7 probed
+    K, f1, f2, iters, B = 40, 3, 10, 3, 1024
+    _, flow = O.synth_batch(K, f1, f2, 0.5, 4343, B)
+    x = torch.from_numpy(flow).to(_dev())
+    with TurboCodec(K, f1, f2, iterations=iters) as c:
+        c.reserve(B)
+        ms, pick = c.placement()
+        _, held = c.placement_cost()
+        ws = c.workspace_bytes()
+        assert len(ms) == 7 and ms[pick] == min(ms)
+        assert ws > 0 and held <= 3 * ws + 4 * (48 << 20), (held, ws)
+        bits = c.decode(x)
+        torch.cuda.synchronize()
+    ob = O.decode_batch(np.ascontiguousarray(flow), K, f1, f2, iters, nthreads=8)
+    assert np.array_equal(bits.cpu().numpy(), ob)
+
+
+def test_reserve_after_a_growing_decode_keeps_the_workspace(monkeypatch):
+    """a decode that grows the workspace (plain allocation), then td_reserve for the
+    same batch: the workspace is big enough, so the reserve neither frees it nor searches."""
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+    monkeypatch.setenv("TD_PLACEMENT_TRIALS", "3")
+    K, B = 40, 1024
+    x = torch.zeros((B, 3 * K + 12), dtype=torch.float64, device=_dev())
+    with TurboCodec(K, 3, 10, iterations=2) as c:
+        c.decode(x)
+        torch.cuda.synchronize()
+        ws = c.workspace_bytes()
+        c.reserve(B)
+        assert c.placement() == ([], -1)
+        assert c.workspace_bytes() == ws
+
+
+def test_set_window_maxstar_rejects_bad_forms():
+    from turbo_decoder_cuda_amd import TurboCodec
+    from turbo_decoder_cuda_amd import _native as N
+    with TurboCodec(40, 3, 10, iterations=2) as c:
+        for form in (-1, 2, 7):
+            with pytest.raises(N.TurboError):
+                N.check(N.lib().td_set_window_maxstar(c._h, form))
+        c.set_window_maxstar(True)
+        c.set_window_maxstar(False)
+
+
 def test_plain_allocation_reports_no_placement(monkeypatch):
     from turbo_decoder_cuda_amd import TurboCodec
     monkeypatch.setenv("TD_PLACEMENT_TRIALS", "1")
