@@ -3384,7 +3384,7 @@ constexpr int sw_seg()
 // its own (and its last ends g steps late), so fewer, longer runs do less work: at config 5 (96
 // sub-blocks, 512 waves of codewords) M = 24 leaves 4 runs a codeword, 2 % extra steps against M = 6's
 // 7.8 %, and 2048 waves a SISO -- one round of the beta kernel's 2048 slots (2 waves a SIMD) over the
-// two halves.  Measured (round 5, same box, TD_WINDOW_RUN): M = 6 2462, 8 2467, 12 2553, 20 2525
+// two halves.  Measured (round 5, same box, forced run lengths, now td_debug_window_layout): M = 6 2462, 8 2467, 12 2553, 20 2525
 // (1.25 rounds), 24 2628, 32 2236 (3/4 of the slots), 48 1559 Mbit/s.
 #ifndef TD_SW_RUN_WAVES
 #define TD_SW_RUN_WAVES 2048
@@ -3433,7 +3433,7 @@ hipError_t launch_window_algo(const DecodeParams<T>& p, const WindowParams& w, c
     a.ckpt[1] = wb.ckpt[1];
     const size_t nii_half = (size_t)2 * a.Bp * nS * 16;
     const int cw_total = a.Bp / 64;
-    // batch parts: 2 by default (TD_WINDOW_PARTS: measured 3 and 4 slower, profiles/r05/sweep_window_layout.txt)
+    // batch parts: 2 by default (td_debug_window_layout: measured 3 and 4 slower, profiles/r05/sweep_window_layout.txt)
     const int want = w.parts > 0 ? min(w.parts, kSwMaxParts) : 2;
     const int nparts = (ws.st[1] && !p.all_iters) ? max(1, min(want, cw_total / kSwHalfWaves)) : 1;
     const bool split = nparts > 1;
