@@ -394,7 +394,10 @@ int place_ws(td_handle* h, int G)
         held += c.total;
         peak = std::max(peak, held);
         s.cand.emplace_back(1e30f, p);
-        const int warm = i == 0 ? 4 : 1;
+        // the first candidate also brings the clocks up: with 4 untimed launches its probe still read
+        // 3-6 % slow (2.11, then 2.06 / 2.06 ms against 1.96-2.03 for the rest; round 6), so a fast
+        // early candidate looked slow and was the first released; 24 launches (~50 ms at config 2) settle them
+        const int warm = i == 0 ? 24 : 1;
         const float ms = h->elem == 8 ? probe_ws<double>(h, static_cast<char*>(p), G, s.st, s.e0, s.e1, warm)
                                       : probe_ws<float>(h, static_cast<char*>(p), G, s.st, s.e0, s.e1, warm);
         s.cand.back().first = ms < 0 ? 1e30f : ms;
