@@ -848,7 +848,48 @@ def variants(a, codec, llr64, u_d, f1, f2, dev, stream):
             res[key]["power"] = prec_pw
     if big is not None and a.K == 6144:
         res["ref_gpu_schedule_P32_10it"] = ref_gpu_schedule(a, big, f1, f2, dev, stream)
+        if a.iters == 8 and a.precision == "f64":
+            res["window_ber_gate"] = window_ber_gate(a, f1, f2, dev)
     return res
+
+
+def window_ber_gate(a, f1, f2, dev, frames=32768, points=(0.35, 0.40), seed=100):
+    """Config 5's BER gate measured in this run (north_star: "BER-vs-Eb/N0 within 0.05 dB of the CPU
+    reference"): the same generator frames at two waterfall points through the exact schedule (bit-exact
+    against the reference) and the windowed one (W = 64, overlap 30, the bench's config-5 line), fp64
+    log-MAP, 8 iterations; the window's shift in dB read through the exact curve's local slope.  The
+    full paired curve is scripts/ber_window_vs_exact.py (profiles/r06/ber_window_vs_exact.json)."""
+    import math
+
+    import torch
+
+    from turbo_decoder_cuda_amd import TurboCodec
+
+    t0 = time.perf_counter()
+    rec = {"frames_per_point": frames, "window": 64, "overlap": a.overlap, "points": []}
+    with TurboCodec(a.K, f1, f2, iterations=a.iters, device=dev.index) as ex, \
+            TurboCodec(a.K, f1, f2, iterations=a.iters, device=dev.index) as win:
+        win.set_window(64, a.overlap)
+        for k, e in enumerate(points):
+            ex.synth_seed(seed + k)
+            info, llr = ex.synth(frames, e)
+            pt = {"ebn0_db": e}
+            for name, c in (("exact", ex), ("window", win)):
+                bits = c.decode(llr)
+                err = (bits != info)
+                pt[f"{name}_bit_errors"] = int(err.sum().item())
+                pt[f"{name}_block_errors"] = int(err.any(dim=1).sum().item())
+                del bits, err
+            rec["points"].append(pt)
+            del info, llr
+    p0, p1 = rec["points"]
+    if min(p0["exact_bit_errors"], p1["exact_bit_errors"], p0["window_bit_errors"], p1["window_bit_errors"]) > 0:
+        slope = math.log(p0["exact_bit_errors"] / p1["exact_bit_errors"]) / (points[1] - points[0])   # ln(BER) per dB
+        rec["shift_db"] = [round(math.log(p["window_bit_errors"] / p["exact_bit_errors"]) / slope, 5)
+                           for p in rec["points"]]
+        rec["within_0.05_db"] = all(abs(x) <= 0.05 for x in rec["shift_db"])
+    rec["wall_s"] = round(time.perf_counter() - t0, 2)
+    return rec
 
 
 def ref_gpu_schedule(a, big, f1, f2, dev, stream, P=32, iters=10):
