@@ -255,6 +255,9 @@ def main():
     elapsed, errs, blk = reduce_over_ranks(t1 - t0, errs, blk, world)
     out = summarize(a, world, elapsed, errs, blk, demux_ms, turbo_ms, nlaunch, f1, f2, clock)
     out["workspace_placement"] = placement_record(placement, turbo_ms, a.iters, placement_cost)
+    if power_rec and power_rec.get("socket_w_mean") and out["value"] > 0:
+        # board energy per decoded info bit over the timed region (socket power / throughput of this GPU)
+        power_rec["nj_per_info_bit"] = round(power_rec["socket_w_mean"] / (out["value"] / world) * 1e3, 2)
     out["power"] = power_rec
 
     if rank == 0 and world == 1 and not a.no_variants:
