@@ -2423,6 +2423,30 @@ __device__ __forceinline__ T sw_mstar(T x, T y, const char* lut)
 // 8-codeword groups; sw_demux_kernel writes this layout.)  Round 4 read the 8-codeword layout: eight
 // 64-byte pieces per wave load, half a cache line each.
 constexpr int kSwCw = 64;
+// cache policy of the windowed kernels' streams (TD_SW_NT bits): 1 checkpoint stores nt, 2 the beta
+// kernel's checkpoint DMA sc0 sc1 nt, 4 its input DMA sc0 sc1 nt, 8 the alpha kernel's input loads nt.
+// The checkpoints are written once and read once, a launch later: kept out of L2 / MALL (3) config 5
+// runs 3410-3415 against 3335-3343 Mbit/s (+2.2 %, one box, 2 interleaved rounds); the inputs, which
+// both kernels read, lose with nt (7: level, 15: -0.5 %; profiles/r06/ab_window_cache_policy.txt)
+#ifndef TD_SW_NT
+#define TD_SW_NT 3
+#endif
+template <typename T>
+__device__ __forceinline__ void sw_ck_store(T* p, T v)
+{
+    if constexpr ((TD_SW_NT & 1) != 0)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+template <int BIT>
+__device__ __forceinline__ void sw_dma(unsigned lds, const void* src)
+{
+    if constexpr ((TD_SW_NT & BIT) != 0)
+        dma16_stream(lds, src);
+    else
+        dma16(lds, src);
+}
 // channel + a-priori of (codeword b, step i) of decoder `dec` (steps outside [0, L) clamped)
 // A wave's 64 codewords are the wide group cwv (wave-uniform) and its lanes, so every address is a
 // wave-uniform base plus the lane: no per-lane 64-bit pointer stays live across the loops (with the
@@ -2434,9 +2458,15 @@ __device__ __forceinline__ SwRaw<T> sw_raw(const DecodeParams<T>& p, const WinAr
     const int ic = min(max(i, 0), p.L - 1);
     const size_t row = (size_t)cwv * p.L + ic, rowk = (size_t)cwv * p.K + min(ic, p.K - 1);
     SwRaw<T> r;
-    r.ys = (dec ? p.sys2 : p.sys1)[row * kSwCw + lane];
-    r.yp = (dec ? p.par2 : p.par1)[row * kSwCw + lane];
-    r.la = a.la[dec][rowk * kSwCw + lane];
+    if constexpr ((TD_SW_NT & 8) != 0) {
+        r.ys = __builtin_nontemporal_load(&(dec ? p.sys2 : p.sys1)[row * kSwCw + lane]);
+        r.yp = __builtin_nontemporal_load(&(dec ? p.par2 : p.par1)[row * kSwCw + lane]);
+        r.la = __builtin_nontemporal_load(&a.la[dec][rowk * kSwCw + lane]);
+    } else {
+        r.ys = (dec ? p.sys2 : p.sys1)[row * kSwCw + lane];
+        r.yp = (dec ? p.par2 : p.par1)[row * kSwCw + lane];
+        r.la = a.la[dec][rowk * kSwCw + lane];
+    }
     return r;
 }
 // the step's P, Q (see "gamma") with La zero where no extrinsic exists (la_ok: i < la_len)
@@ -2698,7 +2728,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
                 T* ck = sw_ck(a, t, s, (bp - st) / S);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    if constexpr (!kDiag<kDiagSwNoCk>) ck[j * 64] = al[j];
+                    if constexpr (!kDiag<kDiagSwNoCk>) sw_ck_store(ck + j * 64, al[j]);
             }
             if (aAll && bAll) {
 #pragma unroll
@@ -2743,7 +2773,7 @@ __global__ __launch_bounds__(256) TD_SW_ALPHA_ATTR void sw_alpha_kernel(DecodePa
                     T* ck = sw_ck(a, t, s, (pos - st) / S);
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if constexpr (!kDiag<kDiagSwNoCk>) ck[j * 64] = al[j];
+                        if constexpr (!kDiag<kDiagSwNoCk>) sw_ck_store(ck + j * 64, al[j]);
                 }
                 if (s < nS - 1 && pos == qb && t.live)
 #pragma unroll
@@ -3118,7 +3148,7 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
             constexpr int kDma = 8 * 64 * (int)sizeof(T) / 1024;
 #pragma unroll
             for (int q = 0; q < kDma; ++q)
-                if constexpr (!kDiag<kDiagSwNoCk>) dma16(ckslot_lds + q * 1024, src + q * 1024);
+                if constexpr (!kDiag<kDiagSwNoCk>) sw_dma<2>(ckslot_lds + q * 1024, src + q * 1024);
         }
         const size_t row = (size_t)cwv * L + nbp, rowk = (size_t)cwv * K + nbp;
         const char* src0 = reinterpret_cast<const char*>((dec ? p.sys2 : p.sys1) + row * kSwCw) + lane * 16;
@@ -3126,9 +3156,9 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
         const char* src2 = reinterpret_cast<const char*>(a.la[dec] + rowk * kSwCw) + lane * 16;
 #pragma unroll
         for (int q = 0; q < kInDma; ++q) {
-            dma16(inslot_lds + q * 1024, src0 + q * 1024);
-            dma16(inslot_lds + S * kRowBytes + q * 1024, src1 + q * 1024);
-            dma16(inslot_lds + 2 * S * kRowBytes + q * 1024, src2 + q * 1024);
+            sw_dma<4>(inslot_lds + q * 1024, src0 + q * 1024);
+            sw_dma<4>(inslot_lds + S * kRowBytes + q * 1024, src1 + q * 1024);
+            sw_dma<4>(inslot_lds + 2 * S * kRowBytes + q * 1024, src2 + q * 1024);
         }
     };
     prefetch(bp);
