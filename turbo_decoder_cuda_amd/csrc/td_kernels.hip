@@ -1495,6 +1495,10 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
 // once per SISO, the window enters only as its ring slots (s3 = t % 3, s4 = t % kAvSlots, s2 = t &
 // 1, kept as running counters by the caller) and its first step i0.  Extrinsic written permuted
 // (ext_mode 2 / 3), no raw-LLR or Le dump (those take fold_item).
+// the folds' extrinsic stores non-temporal (A/B switch; read a SISO later by the loader's tile DMA)
+#ifndef TD_EXT_NT
+#define TD_EXT_NT 0
+#endif
 template <typename T>
 struct FoldLane {
     int k, c;
@@ -1557,7 +1561,12 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
     const T llr = r1 - r0;
     const T le = llr - la - (T)2 * ys;
     const int i = i0 + k;
-    if (i < ext_len) fl.ext[(size_t)wperm * kCw] = le;
+    if (i < ext_len) {
+        if constexpr (TD_EXT_NT != 0)
+            __builtin_nontemporal_store(le, &fl.ext[(size_t)wperm * kCw]);
+        else
+            fl.ext[(size_t)wperm * kCw] = le;
+    }
     if (fl.bits && i < K) fl.bits[wbit] = (llr < (T)0) ? 0 : 1;   // :862-879 at pi[i] (:1264)
 }
 
@@ -2424,7 +2433,8 @@ __device__ __forceinline__ T sw_mstar(T x, T y, const char* lut)
 // 64-byte pieces per wave load, half a cache line each.
 constexpr int kSwCw = 64;
 // cache policy of the windowed kernels' streams (TD_SW_NT bits): 1 checkpoint stores nt, 2 the beta
-// kernel's checkpoint DMA sc0 sc1 nt, 4 its input DMA sc0 sc1 nt, 8 the alpha kernel's input loads nt.
+// kernel's checkpoint DMA sc0 sc1 nt, 4 its input DMA sc0 sc1 nt, 8 the alpha kernel's input loads nt,
+// 16 the beta kernel's extrinsic stores nt.
 // The checkpoints are written once and read once, a launch later: kept out of L2 / MALL (3) config 5
 // runs 3410-3415 against 3335-3343 Mbit/s (+2.2 %, one box, 2 interleaved rounds); the inputs, which
 // both kernels read, lose with nt (7: level, 15: -0.5 %; profiles/r06/ab_window_cache_policy.txt)
@@ -3183,7 +3193,10 @@ __global__ __launch_bounds__(256) TD_SW_BETA_ATTR void sw_beta_kernel(DecodePara
 #pragma unroll
             for (int m = 0; m < S; ++m)
                 if (dst[m] && t.live) {
-                    le[(size_t)dpm[m] * kSwCw + lane] = dlev[m];
+                    if constexpr ((TD_SW_NT & 16) != 0)
+                        __builtin_nontemporal_store(dlev[m], &le[(size_t)dpm[m] * kSwCw + lane]);
+                    else
+                        le[(size_t)dpm[m] * kSwCw + lane] = dlev[m];
                     if (bitsT) bitsT[(size_t)dpk[m] * a.Bp + bcol] = (uint8_t)dbit[m];
                 }
         }
