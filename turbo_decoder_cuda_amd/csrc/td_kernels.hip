@@ -1495,7 +1495,8 @@ __device__ __forceinline__ void fold_item(const Smem<T>& sm, const T* lut, int t
 // once per SISO, the window enters only as its ring slots (s3 = t % 3, s4 = t % kAvSlots, s2 = t &
 // 1, kept as running counters by the caller) and its first step i0.  Extrinsic written permuted
 // (ext_mode 2 / 3), no raw-LLR or Le dump (those take fold_item).
-// the folds' extrinsic stores non-temporal (A/B switch; read a SISO later by the loader's tile DMA)
+// the folds' extrinsic stores non-temporal (A/B switch; read a SISO later by the loader's tile DMA):
+// config 2 level (1514-1516 against 1516-1522 Mbit/s, profiles/r06/ab_extrinsic_nt.txt), not kept
 #ifndef TD_EXT_NT
 #define TD_EXT_NT 0
 #endif
@@ -2437,9 +2438,10 @@ constexpr int kSwCw = 64;
 // 16 the beta kernel's extrinsic stores nt.
 // The checkpoints are written once and read once, a launch later: kept out of L2 / MALL (3) config 5
 // runs 3410-3415 against 3335-3343 Mbit/s (+2.2 %, one box, 2 interleaved rounds); the inputs, which
-// both kernels read, lose with nt (7: level, 15: -0.5 %; profiles/r06/ab_window_cache_policy.txt)
+// both kernels read, lose with nt (7: level, 15: -0.5 %; profiles/r06/ab_window_cache_policy.txt); the
+// extrinsic stores with nt (19) another +1.6 % (3208-3210 against 3157-3160, profiles/r06/ab_extrinsic_nt.txt)
 #ifndef TD_SW_NT
-#define TD_SW_NT 3
+#define TD_SW_NT 19
 #endif
 template <typename T>
 __device__ __forceinline__ void sw_ck_store(T* p, T v)
