@@ -3417,10 +3417,13 @@ __global__ __launch_bounds__(256) void bits_transpose_kernel(const uint8_t* __re
 
 // checkpoint spacing S: the segment's alpha stays in registers.  fp64: 4 (round 4: 2 measured -12 %,
 // 3 and 5 -6 %); fp32: 8.
+#ifndef TD_SW_SEG64
+#define TD_SW_SEG64 4
+#endif
 template <typename T>
 constexpr int sw_seg()
 {
-    return sizeof(T) == 4 ? 8 : 4;
+    return sizeof(T) == 4 ? 8 : TD_SW_SEG64;
 }
 
 // sub-blocks per lane run: one (M = 1) while a launch has fewer than kSwRunWaves one-sub-block waves,
