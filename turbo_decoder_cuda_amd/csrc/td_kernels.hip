@@ -1586,6 +1586,19 @@ __device__ __forceinline__ void fold_item_fast(const FoldLane<T>& fl, const T* l
 // past the last window (kFSkip), so no F-pass DMA is in flight when F1 starts staging.
 template <int ALGO>
 constexpr int kBLoaderWave = ALGO == 1 ? 3 : 2;
+// Max-Log-MAP fold items sorted by recompute depth over the two fold waves (15-step windows; A/B
+// switch TD_ML_DEPTH) and its full windows through fold_item_fast (TD_ML_FAST)
+#ifndef TD_ML_DEPTH
+#define TD_ML_DEPTH 1
+#endif
+#ifndef TD_ML_FAST
+#define TD_ML_FAST 1
+#endif
+template <typename T, int ALGO>
+constexpr bool kMlDepthSplit = TD_ML_DEPTH && ALGO == 1 && kCkPh<ALGO> == 1 && kW == 15 &&
+                               kFoldAOf<T, ALGO> == 64 && kTile - kTile / 3 > kLanes;
+template <typename T, int ALGO>
+constexpr bool kMlFast = TD_ML_FAST && ALGO == 1;
 template <int ALGO>
 constexpr bool kFSkip = kBLoaderWave<ALGO> == 3;   // (on its own, with F0 loading both passes: level)
 constexpr int kAlphaPrio = 2;   // VALU priority of the alpha wave in the F pass
@@ -1966,8 +1979,23 @@ __device__ void siso_wg(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T>& ds
             fe = wave == 0 ? (3 * q + pd) * kCw + (lane & 7) : (3 * (q >> 1) + ((q & 1) ? pb : pa)) * kCw + (lane & 7);
             nfold = wave == 0 ? kTile / 3 : kTile - kTile / 3;
         }
+        if constexpr (kMlDepthSplit<T, ALGO>) {
+            // 15-step windows, Max-Log-MAP (phase 0 kept): 40 items of each recompute depth.  Wave A
+            // takes the 40 depth-2 items (steps 2, 5, .., 14) and 24 of depth 1 (steps 1, 4, 7), the
+            // other fold wave the remaining 16 of depth 1 (steps 10, 13) and the 40 of depth 0
+            // (steps 0, 3, .., 12), so it runs one recompute step instead of two (in step order both
+            // waves held lanes of every depth, and the divergent loop ran twice in both)
+            const int l = lane;
+            int k;
+            if (wave == 0)
+                k = l < 40 ? 3 * (l >> 3) + 2 : 3 * ((l - 40) >> 3) + 1;
+            else
+                k = l < 16 ? 3 * (3 + (l >> 3)) + 1 : 3 * (min(l - 16, 39) >> 3);
+            fe = k * kCw + (l & 7);
+            nfold = wave == 0 ? 64 : 56;
+        }
         int j0 = 0;
-        if (ALGO == 0 && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
+        if ((ALGO == 0 || kMlFast<T, ALGO>) && !dst.llr && !dst.le_dump && dst.ext_mode >= 2 && tl >= 1) {
             // iterations 0, 1 fold nothing, 2 folds the last window (maybe partial): generic below;
             // here iterations 3 .. nB-1, i.e. the full windows wf = tl-1 .. 0
             for (int j = 0; j < 3; ++j) {
