@@ -53,7 +53,7 @@ for w in range(NW):
           + (f"  F prologue {s[:, w, 11].mean() / steps:6.1f}" if NS > 11 else "")
           + (f"  B prologue {s[:, w, 12].mean() / steps:6.1f}  first tile {s[:, w, 13].mean() / steps:6.1f}" if NS > 13 and w == 2 else "")
           + (f"  B convert {s[:, w, 14].mean() / steps:6.1f}  DMA wait {s[:, w, 4].mean() / steps:6.1f}  tm_from_alpha "
-             f"{s[:, w, 15].mean() / steps:6.1f}" if NS > 15 and w == 2 else ""))
+             f"{s[:, w, 15].mean() / steps:6.1f}" if NS > 15 and w in (2, 3) else ""))
 hw = st.cpu().numpy().reshape(G, NW, NS)[:, :, 6].astype(np.int64)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15

@@ -662,16 +662,31 @@ __device__ __forceinline__ void tm_dma(Smem<T>& sm, int slot, const T* tmstore, 
         dma16(lds_addr(&sm.stage[3][slot * kTmStageBytes<T>]), tmstore + ((size_t)gm.g * gm.L + i) * kCw + (e0 & 7));
 }
 
-// staged tempmax of window t -> its LDS slot (beta input)
+// staged tempmax of window t -> its LDS slot (beta input; Max-Log-MAP's B-pass loader).  Batched
+// reads (TD_TM_CONVERT_BATCH, fp64): config 3 2380-2389 -> 2399-2404 Mbit/s (+0.8 %, 3 rounds); fp32
+// Max-Log-MAP lost 1.3 % with it and keeps the masked form (profiles/r06/ab_maxlog_tm_convert.txt)
+#ifndef TD_TM_CONVERT_BATCH
+#define TD_TM_CONVERT_BATCH 1
+#endif
 template <typename T>
 __device__ __forceinline__ void tm_convert(Smem<T>& sm, int slot, int t, int lane)
 {
     const T* sv = reinterpret_cast<const T*>(&sm.stage[3][slot * kTmStageBytes<T>]);
     T* d = &sm.tm[t & 1][0][0];
+    if constexpr (TD_TM_CONVERT_BATCH != 0 && kW == 15 && sizeof(T) == 8) {
+        // both reads before the first write and no lane masked (as tile_convert): lanes past the window
+        // repeat its last element, the same value to the same address.  (The 12-step build is left as
+        // it was: with this form its TU hits an instruction-selection error in the compiler.)
+        const int e0 = lane, e1 = min(lane + kLanes, kTile - 1);
+        const T v0 = sv[e0], v1 = sv[e1];
+        d[e0] = v0;
+        d[e1] = v1;
+    } else {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = lane + kLanes * q;
-        if (e < kTile) d[e] = sv[e];
+        for (int q = 0; q < 2; ++q) {
+            const int e = lane + kLanes * q;
+            if (e < kTile) d[e] = sv[e];
+        }
     }
 }
 
@@ -1696,6 +1711,8 @@ __device__ void bpass_loader(Smem<T>& sm, const SisoSrc<T>& src, const SisoDst<T
             if (wa >= 0) tm_convert(sm, slot, wa, lane);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's reads are done before it is re-staged
+        TD_STAMP(bc);
+        TD_ACC(14, b0, bc);   // stamps build: the loader's slot 14 is its B-pass conversion (tiles + tempmax)
         tile_dma(sm, slot, src, dst, gm, max(min(wa - 3, tl - 3), 0), lane);
         tm_dma(sm, slot, tmstore, gm, wa - 3, lane);
         if constexpr (kAd > 0) alpha_dma<T, ALGO>(sm, astore, gm, wa - 1, lane);
